@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident Mpkt/s of XDP-emulator verdicts (BASELINE.json metric).
+
+Default workload (N=1) = BASELINE configs[1], "C2": ~40-insn L2/L3 classifier over 16,777,216 x 64 B
+synthetic packets with per-proto ARRAY counters. A step = one pass of the batch through the emulator
+(xe_run_batch_device: map snapshot, interpreter kernel, commutativity check) with packets, descriptors
+and the verdict buffer already resident in HBM. For N>1 (torchrun, one rank per GPU) every rank runs
+its own 16M-packet shard (weak scaling) and the counter map deltas are all-reduced over RCCL inside
+the step. Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--packets P]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0
+WORKLOADS = {
+    "c2": "C2 (BASELINE configs[1]): ~40-insn L2/L3 parse->PASS/DROP classifier, per-proto ARRAY counters",
+    "c3": "C3: 5-tuple HASH lookup -> REDIRECT + hit counter, 64K flows, IMIX 64/576/1500 B",
+    "c4": "C4: ~200-insn JEQ/JGT ACL (48 rules), 1500 B packets, lane-divergence stress",
+    "c5": "C5: C2 parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets",
+}  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec peak
+
+
+def alg_bytes_per_packet(sizes: np.ndarray) -> np.ndarray:
+    """16 B descriptor + min(len, 64) header window + 4 B verdict."""
+    return 16 + np.minimum(sizes, 64) + 4
+
+
+def cpu_baseline(name: str, n_sample: int) -> dict:
+    """The oracle (C++ restatement of emulator/, one thread) timed on a bounded prefix of the workload."""
+    from gobpfld_amd import _native as N
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd import build as B
+    B.build_oracle()
+    vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
+    W.setup_vm(vm, name)
+    umem, descs = W.build_batch(name, 0, n_sample)
+    t0 = time.perf_counter()
+    r = vm.run_batch(umem, descs)
+    dt = time.perf_counter() - t0
+    vm.close()
+    return {"value": round(n_sample / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+            "sample": f"first {n_sample} packets of {name} through oracle/liboracle.so (C++ restatement of "
+                      f"gobpfld emulator/, single thread, per-packet Reset/Run harness); {dt:.2f} s; "
+                      f"{r.stats['steps'] / n_sample:.1f} insns/pkt"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="oracle baseline sample (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import VM, Settings
+
+    name = args.config
+    n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))
+    if name == "c5" and not args.packets:
+        n = W.CONFIGS["c5"]["n"] // 8  # 33,554,432 per GPU
+    start = rank * n
+
+    # ---- inputs resident in HBM (synthetic packets; shard = contiguous packet index range)
+    umem, descs = W.build_batch(name, start, n)
+    sizes = descs["len"].astype(np.int64)
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
+    d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    del umem
+
+    vm = VM(Settings(device=local))
+    W.setup_vm(vm, name)
+    maps = list(vm.map_defs)
+    deltas = {m: torch.zeros(vm.map_values_bytes(m) // 8, dtype=torch.int64, device=dev) for m in maps}
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step() -> dict:
+        st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
+                                 d_verdicts=d_ver.data_ptr(), stream=stream)
+        if world > 1:
+            for m in maps:  # counter deltas -> RCCL all-reduce (sum, u64 wrap) -> every replica
+                vm.map_delta(m, deltas[m].data_ptr(), stream=stream)
+                dist.all_reduce(deltas[m])
+                vm.map_apply_delta(m, deltas[m].data_ptr(), stream=stream)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kernel_ms, mode, conflicts, steps_retired, status_ok = [], set(), 0, 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        kernel_ms.append(st["kernel_ms"])
+        mode.add(st["mode_used"])
+        conflicts += st["conflict"]
+        steps_retired += st["steps"]
+        status_ok += st["status_count"][0]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    total_pkts = n * world * args.steps
+    value = total_pkts / elapsed / 1e6
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    bytes_per_launch = float(alg_bytes_per_packet(sizes).sum())
+    achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
+    insns_per_pkt = steps_retired / max(1, n * args.steps)
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            sample = args.cpu_sample or (200_000 if name != "c4" else 100_000)
+            cpu = cpu_baseline(name, sample)
+        hw = {"c2": "64B", "c3": "IMIX 64/576/1500B", "c4": "1500B", "c5": "64B"}.get(name, "64B")
+        out = {
+            "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches",
+            "value": round(value, 3),
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (deterministic splitmix64 packets, SURVEY §8d)",
+            "config": {"workload": WORKLOADS[name],
+                       "packets_per_gpu": n, "packet_size": hw, "parallelism": f"dp{world} (packet shards)",
+                       "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
+                       "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "alg_bytes_per_launch": int(bytes_per_launch),
+                         "alg_bytes_per_packet": "16 desc + min(len,64) header + 4 verdict"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    vm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

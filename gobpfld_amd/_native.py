@@ -1,0 +1,124 @@
+"""ctypes binding of the C ABI declared in include/xdpemu.h.
+
+The same binding drives three libraries with identical signatures: the product
+(gobpfld_amd/libxdpemu.so, prefix ``xe_``), and — in tests only — the CPU oracle
+(oracle/liboracle.so, prefix ``orc_``) and the host simulation of the device logic.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PRODUCT_LIB = ROOT / "gobpfld_amd" / "libxdpemu.so"
+
+
+class Desc(C.Structure):  # xsk.go:695-701
+    _fields_ = [("addr", C.c_uint64), ("len", C.c_uint32), ("options", C.c_uint32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("status", C.c_uint8), ("r0_kind", C.c_uint8), ("code", C.c_uint16),
+                ("pc", C.c_uint32), ("r0", C.c_int64)]
+
+
+class Regs(C.Structure):
+    _fields_ = [("val", C.c_int64 * 10), ("kind", C.c_uint8 * 10), ("region", C.c_uint8 * 10),
+                ("map", C.c_uint8 * 10), ("pad", C.c_uint8 * 2), ("steps", C.c_uint32)]
+
+
+class MapDef(C.Structure):  # map_definition.go:15-27
+    _fields_ = [("type", C.c_uint32), ("key_size", C.c_uint32), ("value_size", C.c_uint32),
+                ("max_entries", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Settings(C.Structure):  # emulator/vm.go:282-296 + device knobs
+    _fields_ = [("stack_frame_size", C.c_int32), ("max_stack_frames", C.c_int32),
+                ("max_steps", C.c_uint64), ("ingress_ifindex", C.c_uint32),
+                ("rx_queue_index", C.c_uint32), ("device", C.c_int32), ("mode", C.c_uint32)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("packets", C.c_uint64), ("steps", C.c_uint64), ("status_count", C.c_uint64 * 8),
+                ("mode_used", C.c_uint32), ("conflict", C.c_uint32), ("kernel_ms", C.c_float),
+                ("total_ms", C.c_float)]
+
+
+# numpy dtypes matching the structs (for zero-copy batch buffers)
+def np_dtypes():
+    import numpy as np
+    desc = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
+    result = np.dtype([("status", "u1"), ("r0_kind", "u1"), ("code", "<u2"), ("pc", "<u4"), ("r0", "<i8")])
+    regs = np.dtype([("val", "<i8", (10,)), ("kind", "u1", (10,)), ("region", "u1", (10,)),
+                     ("map", "u1", (10,)), ("pad", "u1", (2,)), ("steps", "<u4")], align=True)
+    assert desc.itemsize == 16 and result.itemsize == 16 and regs.itemsize == C.sizeof(Regs)
+    return desc, result, regs
+
+
+P = C.c_void_p
+_SIGS = {
+    "default_settings": (C.c_int, [P]),
+    "create": (C.c_int, [P, C.POINTER(P)]),
+    "destroy": (None, [P]),
+    "last_error": (C.c_char_p, [P]),
+    "add_raw_program": (C.c_int, [P, P, C.c_uint32, C.POINTER(C.c_int32)]),
+    "set_entrypoint": (C.c_int, [P, C.c_int32]),
+    "add_map": (C.c_int, [P, P, P, C.c_size_t, C.POINTER(C.c_int32)]),
+    "map_lookup": (C.c_int, [P, C.c_int32, P, P]),
+    "map_update": (C.c_int, [P, C.c_int32, P, P]),
+    "map_delete": (C.c_int, [P, C.c_int32, P]),
+    "map_count": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
+    "map_dump": (C.c_int, [P, C.c_int32, P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "run_batch": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),  # oracle form
+    "run_batch_host": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),
+    "run_batch_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
+    "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
+    "map_delta": (C.c_int, [P, C.c_int32, P, P]),
+    "map_apply_delta": (C.c_int, [P, C.c_int32, P, P]),
+    "footprint": (C.c_int, [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "version": (C.c_char_p, []),
+    "device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "decode_names": (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t]),
+}
+
+# every symbol include/xdpemu.h declares (checked by tests/test_abi.py)
+HEADER_SYMBOLS = [
+    "xe_default_settings", "xe_create", "xe_destroy", "xe_last_error", "xe_add_raw_program",
+    "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
+    "xe_map_count", "xe_map_dump", "xe_run_batch_device", "xe_run_batch_host",
+    "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_footprint", "xe_version",
+    "xe_device_count",
+]
+
+
+class Lib:
+    """A loaded emulator library exposing the xdpemu.h calls without their prefix."""
+
+    def __init__(self, path: Path | str, prefix: str = "xe_"):
+        self.path = Path(path)
+        if not self.path.exists():
+            raise FileNotFoundError(
+                f"{self.path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        self.dll = C.CDLL(str(self.path))
+        self.prefix = prefix
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(self.dll, prefix + name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name, fn)
+
+    def has(self, name: str) -> bool:
+        return hasattr(self, name)
+
+
+_product: Lib | None = None
+
+
+def product() -> Lib:
+    """The HIP product library. Raises if it is not built — there is no CPU fallback."""
+    global _product
+    if _product is None:
+        _product = Lib(PRODUCT_LIB, "xe_")
+    return _product

@@ -1,0 +1,142 @@
+// xe_internal.h — shared host/device definitions of the batched eBPF/XDP emulator.
+//
+// Micro-op table (host translator -> device interpreter), per-lane memory handles, the device
+// map descriptors and the hash-table layout. Portable between hipcc (device + host) and g++ (the
+// test-only host simulation build, XE_HOSTSIM).
+#pragma once
+#include <stdint.h>
+#include "../../include/xdpemu.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define XE_HD __host__ __device__ __forceinline__
+#else
+#define XE_HD static inline
+#endif
+
+// ---------------------------------------------------------------- micro-ops
+// One 16-byte record per eBPF instruction slot (the LD_IMM64 filler keeps its own slot, exactly
+// as ebpf.Decode emits a Nop, ebpf/decode.go:34), so PCs stay identical to the reference's.
+enum XeUopClass : uint8_t {
+  U_FAIL = 0,   // statically determined error: imm = (status << 16) | code
+  U_NOP,        // emulator/inst_nop.go
+  U_EXIT,       // emulator/inst_exit.go
+  U_JA,         // emulator/inst_ja.go
+  U_ALU,        // x = BPF op nibble; fl: WIDE, REG
+  U_MOVI,       // emulator/inst_mov.go:20-46
+  U_MOVR,       // emulator/inst_mov.go:60-99
+  U_NEG,        // emulator/inst_neg.go
+  U_END,        // emulator/inst_end.go; x = 0 (to_le) / 8 (to_be); imm = 16/32/64
+  U_JMP,        // x = BPF jmp op nibble; fl: WIDE (64-bit compare), REG
+  U_LDIMM64,    // emulator/inst_load.go:21-71; src = pseudo src; imm = Val1; x = Val2
+  U_LDX,        // emulator/inst_load.go:84-118
+  U_ST,         // emulator/inst_store.go:20-51
+  U_STX,        // emulator/inst_store.go:64-99
+  U_ATOMIC,     // emulator/inst_atomic.go:20-65
+  U_HELPER,     // CallHelper with a known helper id (imm)
+  U_CALLX,      // CallHelperIndirect; dst = register holding the helper id
+  U_CALLBPF,    // bpf-to-bpf call (device: XE_ST_UNSUPPORTED in this round)
+  U_NCLASSES
+};
+
+enum : uint8_t {
+  UF_WIDE = 1,       // 64-bit ALU / JMP
+  UF_REG = 2,        // BPF_X form
+  UF_BADDST = 4,     // LDX: Assign(dst) will fail after the read (dst > 9)
+  UF_BADSRC = 8,     // ATOMIC: Get(src) will fail after the read (src > 9)
+};
+
+struct XeUop {
+  uint8_t cls;
+  uint8_t dst;
+  uint8_t src;
+  uint8_t fl;    // UF_* | (size_log2 << 4) for memory ops
+  int32_t imm;
+  int32_t tgt;   // jumps: PC after the jump is taken (pc + off), i.e. before the +1 of Step
+  uint32_t x;
+};
+static_assert(sizeof(XeUop) == 16, "uop must be 16 bytes (one s_load_dwordx4)");
+
+XE_HD int uop_size(const XeUop& u) { return 1 << ((u.fl >> 4) & 3); }
+
+// ---------------------------------------------------------------- memory handles
+// A pointer register's Memory is encoded in 32 bits: class (3) | map index (6) | slot (23).
+#define XE_H_CLS_SHIFT 29
+#define XE_H_PKT 0u
+#define XE_H_CTX 1u
+#define XE_H_STACK 2u
+#define XE_H_ARRAY 3u
+#define XE_H_HASH 4u
+#define XE_H_MAX_MAPS 63
+#define XE_H_SLOT_BITS 23
+XE_HD uint32_t xe_h_make(uint32_t cls, uint32_t map, uint32_t slot) {
+  return (cls << XE_H_CLS_SHIFT) | (map << XE_H_SLOT_BITS) | slot;
+}
+XE_HD uint32_t xe_h_cls(uint32_t h) { return h >> XE_H_CLS_SHIFT; }
+XE_HD uint32_t xe_h_map(uint32_t h) { return (h >> XE_H_SLOT_BITS) & 63u; }
+XE_HD uint32_t xe_h_slot(uint32_t h) { return h & ((1u << XE_H_SLOT_BITS) - 1u); }
+
+// ---------------------------------------------------------------- device maps
+enum : uint32_t { XE_DM_NONE = 0, XE_DM_ARRAY = 1, XE_DM_HASH = 2, XE_DM_OTHER = 3 };
+#define XE_SLOT_FULL 1u
+#define XE_SLOT_VLEN0 2u   // HashMap value whose backing became nil (maps_hash.go:108-115)
+#define XE_MAX_KEY 64      // device hash keys up to 64 bytes (8 words)
+
+struct XeDevMap {
+  uint32_t kind;        // XE_DM_*
+  uint32_t key_size;
+  uint32_t value_size;
+  uint32_t max_entries;
+  uint64_t vals_bytes;  // ARRAY: value_size*max_entries; HASH: (cap+1)*value_size
+  uint8_t* vals;        // ARRAY memory / HASH slot values (slot cap = the nil-key slot)
+  uint64_t* keys;       // HASH: (cap+1) * kwords u64 words, zero padded
+  uint32_t* state;      // HASH: (cap+1) slot states
+  uint32_t* count;      // HASH: number of entries (device word)
+  uint32_t cap;         // HASH: power-of-two slot count
+  uint32_t kwords;      // HASH: (key_size+7)/8
+};
+
+// Word-wise multiplicative hash over the zero-padded key words. The reference hashes with sha256
+// (maps_hash.go:55); the function is unobservable (only key equality matters), so a cheap one is
+// used. Host and device compute the identical slot layout.
+XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_size) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t(key_size) * 0xC2B2AE3D27D4EB4Full);
+  for (uint32_t i = 0; i < nwords; i++) {
+    h ^= w[i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  h ^= h >> 29;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 32;
+  return h;
+}
+
+// kernel-side status of a lane beyond the public XE_ST_*
+#define XE_ST_INTERNAL_ORDERED 6
+
+// flags word bits (device -> host)
+#define XE_FLAG_ORDERED 1u   // a lane needed a non-commutative map write in parallel mode
+#define XE_FLAG_CAPACITY 2u
+
+// per-launch parameters
+struct XeParams {
+  const XeUop* prog;
+  int32_t prog_len;
+  uint32_t mode;          // XE_MODE_PARALLEL or XE_MODE_SEQUENTIAL
+  uint8_t* umem;
+  uint64_t umem_len;
+  const xe_desc* desc;
+  uint32_t n;
+  uint32_t nmaps;         // len(vm.Maps) - 1
+  xe_result* results;
+  uint32_t* verdicts;
+  xe_regs* regs;
+  const XeDevMap* maps;   // [0..nmaps], index 0 unused
+  uint64_t max_steps;
+  uint32_t ingress;
+  uint32_t rxq;
+  uint32_t* flags;             // XE_FLAG_*
+  unsigned long long* fp;      // [(nmaps+1)*2]: read mask, atomic mask per map
+  unsigned long long* stats;   // [0] steps, [1..8] status histogram
+};

@@ -1,0 +1,965 @@
+// xe_interp.h — the batched eBPF/XDP interpreter core.
+//
+// One lane interprets one packet. The 64 lanes of a wave share one micro-op stream: each step the
+// wave picks the minimum PC among its running lanes (ballot + readlane; uniform fast path), fetches
+// that micro-op with a scalar load and executes it on the lanes sitting at that PC. Forward branches
+// dominate XDP programs, so diverged lanes re-converge at join points.
+//
+// Register/memory model — an exact encoding of gobpfld's object model (emulator/registers.go,
+// emulator/memory.go):
+//   * R0..R10 live in VGPR arrays indexed by the (wave-uniform) micro-op fields: value (i64),
+//     memory handle (u32) and a tag (kind | readonly | alias id).
+//   * Objects stored in a ValueMemory (the 24-byte xdp_md ctx and the 256-byte stack frame) live in
+//     a per-lane object table (ids 1..63); ValueMemory bytes hold object ids (0 = nil).
+//   * LDX from a ValueMemory makes the register alias the stored object (emulator/memory.go:37-52,
+//     emulator/inst_load.go:112); in-place ALU ops on an aliased register update the object and
+//     every other register aliasing it, exactly like mutating the shared Go object.
+//   * Stack/ctx byte maps reset lazily with a dirty-word mask (Reset nils 2,048 slots per packet,
+//     emulator/vm.go:229-239; here one VGPR write).
+//
+// Maps: ARRAY memory and HASH slot values are device-global. In parallel mode only commutative map
+// effects are executed (atomic adds); a lane that would perform a non-atomic map write aborts the
+// batch (XE_FLAG_ORDERED) and the host re-runs it in exact packet order (sequential mode). Lanes
+// record read / atomic footprints per map so the host can verify order-independence.
+//
+// The same source builds the gfx950 kernel (xe_kernel.hip) and, with XE_HOSTSIM, a wave-size-1 host
+// simulation used only by CPU tests to exercise this logic before it reaches the GPU.
+#pragma once
+#include "xe_internal.h"
+
+#if defined(__HIPCC__)
+#define XE_DEV __device__ __forceinline__
+#define XE_WAVE 64
+XE_DEV unsigned long long xe_ballot(bool p) { return __ballot(p); }
+XE_DEV int xe_readfirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+XE_DEV int xe_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+XE_DEV int xe_lane() { return __lane_id(); }
+XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return atomicAdd(p, v); }
+XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { return atomicCAS(p, c, v); }
+XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { atomicOr(p, v); }
+XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) { atomicOr(p, v); }
+XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return atomicAdd(p, v); }
+XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#else
+#define XE_DEV static inline
+#define XE_WAVE 1
+XE_DEV unsigned long long xe_ballot(bool p) { return p ? 1ull : 0ull; }
+XE_DEV int xe_readfirst(int v) { return v; }
+XE_DEV int xe_readlane(int v, int) { return v; }
+XE_DEV int xe_lane() { return 0; }
+XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { __atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); return c; }
+XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
+XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
+XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+#endif
+
+// kernel-internal error encoding
+#define XE_EV_PANIC 0x1000
+#define XE_EV_UNSUP 0x2000
+#define XE_EV_CAP 0x3000
+#define XE_EV_ORD 0x4000
+#define XE_EV_EXIT 0x8000
+#define XE_EV_CLASS(e) ((e) & 0xf000)
+#define XE_IS_PANIC(e) (XE_EV_CLASS(e) == XE_EV_PANIC)
+
+#define XE_NOBJ 64
+#define XE_STACK_WORDS 32   // 256-byte frame 0
+#define XE_CTX_WORD0 32     // ctx bytes 0..23 = words 32..34
+#define XE_NWORDS 35
+#define XE_CTX_LEN 24
+
+// tag layout
+#define XE_T_KIND(t) ((t) & 3u)
+#define XE_T_RO 4u
+#define XE_T_ALIAS(t) (((t) >> 8) & 63u)
+
+XE_DEV int64_t xe_wadd(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
+XE_DEV int64_t xe_wmul(int64_t a, int64_t b) { return int64_t(uint64_t(a) * uint64_t(b)); }
+XE_DEV int32_t xe_i32(int64_t v) { return int32_t(uint32_t(uint64_t(v))); }
+
+// default ctx words: bytes 0-3 object 1 (data), 4-7 object 2 (data_end), ... 20-23 object 6
+XE_DEV uint64_t xe_ctx_default_word(int w) {
+  return w == XE_CTX_WORD0 ? 0x0202020201010101ull
+       : w == XE_CTX_WORD0 + 1 ? 0x0404040403030303ull
+       : 0x0606060605050505ull;
+}
+
+struct XeLane {
+  // registers R0..R10
+  int64_t rv[11];
+  uint32_t rh[11];
+  uint32_t rt[11];
+  // object table (ids 1..63; 1..6 are the ctx objects, materialised lazily)
+  int64_t ov[XE_NOBJ];
+  uint32_t oh[XE_NOBJ];
+  uint32_t ot[XE_NOBJ];
+  uint64_t oused;     // allocated ids
+  uint64_t odef;      // ids 1..6 still holding their ctx default
+  // ValueMemory byte maps (ids), lazily reset
+  uint64_t bm[XE_NWORDS];
+  uint64_t dirty;
+  // packet
+  uint8_t* pkt;
+  int64_t plen;
+  // per-lane map footprints for maps 1..4 (others go straight to global)
+  uint64_t fpr[4];
+  uint64_t fpa[4];
+};
+
+// ------------------------------------------------------------------ object table
+XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& t) {
+  if ((L.odef >> id) & 1ull) {
+    // xdp_md objects: data, data_end, data_meta = MemoryPtr{pkt}, then 3 IMMs
+    h = id <= 3 ? xe_h_make(XE_H_PKT, 0, 0) : 0u;
+    t = id <= 3 ? uint32_t(XE_KIND_MEMPTR) : uint32_t(XE_KIND_IMM);
+    v = id == 2 ? L.plen : 0;  // ingress/rxq filled by the caller through ov[] defaults below
+    return;
+  }
+  v = L.ov[id];
+  h = L.oh[id];
+  t = L.ot[id];
+}
+
+XE_DEV void obj_set(XeLane& L, int id, int64_t v, uint32_t h, uint32_t t) {
+  L.ov[id] = v;
+  L.oh[id] = h;
+  L.ot[id] = t;
+  L.odef &= ~(1ull << id);
+}
+
+// in-place value update of object `id` (RegisterValue.Assign on a shared object)
+XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
+  if ((L.odef >> id) & 1ull) {
+    int64_t ov; uint32_t oh, ot;
+    obj_get(L, id, ov, oh, ot);
+    obj_set(L, id, v, oh, ot);
+  } else {
+    L.ov[id] = v;
+  }
+}
+
+XE_DEV uint64_t bm_word(const XeLane& L, int w) {
+  if ((L.dirty >> w) & 1ull) return L.bm[w];
+  return w >= XE_CTX_WORD0 ? xe_ctx_default_word(w) : 0ull;
+}
+XE_DEV void bm_set_word(XeLane& L, int w, uint64_t v) {
+  L.bm[w] = v;
+  L.dirty |= 1ull << w;
+}
+
+// mark-sweep collection of object ids when the table is full
+XE_DEV void obj_gc(XeLane& L) {
+  uint64_t marks = 1ull;
+  for (int w = 0; w < XE_NWORDS; w++) {
+    uint64_t word = bm_word(L, w);
+    for (int b = 0; b < 8; b++) marks |= 1ull << ((word >> (8 * b)) & 63u);
+  }
+  for (int r = 0; r < 10; r++) {
+    uint32_t a = XE_T_ALIAS(L.rt[r]);
+    if (a) marks |= 1ull << a;
+  }
+  marks |= 1ull;
+  L.oused = marks;
+}
+
+XE_DEV int obj_alloc(XeLane& L) {
+  if (L.oused == ~0ull) obj_gc(L);
+  if (L.oused == ~0ull) return -1;
+  int id = __builtin_ctzll(~L.oused);
+  L.oused |= 1ull << id;
+  return id;
+}
+
+// ------------------------------------------------------------------ registers
+XE_DEV void reg_replace(XeLane& L, int d, uint32_t kind, uint32_t h, int64_t v, uint32_t alias_and_ro) {
+  L.rv[d] = v;
+  L.rh[d] = h;
+  L.rt[d] = kind | alias_and_ro;
+}
+
+// RegisterValue.Assign on register d's object (in place; registers.go:194-197,243-247,305-313)
+XE_DEV int reg_inplace(XeLane& L, int d, int64_t v) {
+  uint32_t t = L.rt[d];
+  if (XE_T_KIND(t) == XE_KIND_FRAMEPTR && (t & XE_T_RO)) return XE_E_READONLY;
+  L.rv[d] = v;
+  uint32_t a = XE_T_ALIAS(t);
+  if (a) {
+    obj_set_val(L, int(a), v);
+#pragma unroll
+    for (int j = 0; j < 10; j++)
+      if (XE_T_ALIAS(L.rt[j]) == a) L.rv[j] = v;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ footprints
+XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
+  uint64_t vs = M.value_size;
+  if (vs == 0) return ~0ull;
+  uint64_t o = array ? uint64_t(off) % vs : uint64_t(off);
+  uint64_t e = o + uint64_t(size);  // exclusive
+  if (e > vs) return ~0ull;         // straddles two values
+  uint64_t lo, hi;
+  if (vs <= 64) { lo = o; hi = e - 1; }
+  else { lo = o * 64 / vs; hi = (e - 1) * 64 / vs; }
+  uint64_t top = hi >= 63 ? ~0ull : ((1ull << (hi + 1)) - 1ull);
+  return top & ~((1ull << lo) - 1ull);
+}
+
+XE_DEV void fp_record(XeLane& L, const XeParams& P, uint32_t m, bool atomic, uint64_t bits) {
+  if (m >= 1 && m <= 4) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (uint32_t(k + 1) == m) {
+        if (atomic) L.fpa[k] |= bits; else L.fpr[k] |= bits;
+      }
+    }
+  } else {
+    xe_atomic_or64(&P.fp[m * 2 + (atomic ? 1 : 0)], bits);
+  }
+}
+
+// ------------------------------------------------------------------ ByteMemory access
+struct XeBMem {
+  uint8_t* base;
+  int64_t len;
+  uint32_t map;     // 0 = packet
+  bool array;
+};
+
+XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem& B) {
+  uint32_t c = xe_h_cls(h);
+  if (c == XE_H_PKT) { B.base = L.pkt; B.len = L.plen; B.map = 0; B.array = false; return true; }
+  uint32_t m = xe_h_map(h);
+  const XeDevMap& M = P.maps[m];
+  B.map = m;
+  if (c == XE_H_ARRAY) { B.base = M.vals; B.len = int64_t(M.vals_bytes); B.array = true; return true; }
+  uint32_t slot = xe_h_slot(h);
+  B.base = M.vals + uint64_t(slot) * M.value_size;
+  B.len = (M.state[slot] & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
+  B.array = false;
+  return true;
+}
+
+// Go bounds check with wrapping add; passing the check with off >= len (overflow) panics at the index
+XE_DEV int bounds(int64_t off, int64_t size, int64_t len) {
+  if (off < 0 || xe_wadd(off, size) > len) return XE_E_OOB;
+  if (off >= len && size > 0) return XE_EV_PANIC | XE_P_INDEX;
+  return 0;
+}
+
+XE_DEV uint64_t load_le(const uint8_t* p, int size) {
+  uintptr_t a = uintptr_t(p);
+  if ((a & uintptr_t(size - 1)) == 0) {
+    switch (size) {
+      case 1: return *p;
+      case 2: return *reinterpret_cast<const uint16_t*>(p);
+      case 4: return *reinterpret_cast<const uint32_t*>(p);
+      default: return *reinterpret_cast<const uint64_t*>(p);
+    }
+  }
+  uint64_t x = 0;
+  for (int b = 0; b < size; b++) x |= uint64_t(p[b]) << (8 * b);
+  return x;
+}
+
+XE_DEV void store_le(uint8_t* p, int size, uint64_t x) {
+  uintptr_t a = uintptr_t(p);
+  if ((a & uintptr_t(size - 1)) == 0) {
+    switch (size) {
+      case 1: *p = uint8_t(x); return;
+      case 2: *reinterpret_cast<uint16_t*>(p) = uint16_t(x); return;
+      case 4: *reinterpret_cast<uint32_t*>(p) = uint32_t(x); return;
+      default: *reinterpret_cast<uint64_t*>(p) = x; return;
+    }
+  }
+  for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
+}
+
+// Atomic little-endian add of `add` into the `size`-byte field at p (any alignment), truncating
+// at the field's top byte exactly like a read/add/write of that width (inst_atomic.go:44-59). Each
+// 32-bit word is updated with a CAS on its masked bytes; the carry out of a word's slice feeds the
+// next word's add, so the sum over all lanes is exact whatever the interleaving.
+XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
+  uintptr_t a = uintptr_t(p);
+  if (size == 8 && (a & 7) == 0) { xe_atomic_add64(reinterpret_cast<unsigned long long*>(p), add); return; }
+  if (size == 4 && (a & 3) == 0) { xe_atomic_add32(reinterpret_cast<unsigned int*>(p), uint32_t(add)); return; }
+  uintptr_t start = a, end = a + uintptr_t(size);
+  uint64_t carry = 0;
+  uintptr_t w = start & ~uintptr_t(3);
+  int consumed = 0;  // field bytes consumed so far
+  while (w < end) {
+    int lo = start > w ? int(start - w) : 0;
+    int hi = end < w + 4 ? int(end - w) : 4;  // exclusive
+    int nb = hi - lo;
+    uint32_t mask = (nb == 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u)) << (8 * lo);
+    uint64_t part = (consumed < 8 ? (add >> (8 * consumed)) : 0) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1ull));
+    uint64_t addend = part + carry;  // may exceed the slice width by one carry bit
+    unsigned int* wp = reinterpret_cast<unsigned int*>(w);
+    unsigned int old = *wp, assumed;
+    uint64_t sum;
+    do {
+      assumed = old;
+      uint64_t cur = (uint64_t(assumed) & mask) >> (8 * lo);
+      sum = cur + addend;
+      uint32_t nw = (assumed & ~mask) | (uint32_t(sum << (8 * lo)) & mask);
+      old = xe_atomic_cas32(wp, assumed, nw);
+    } while (old != assumed);
+    carry = sum >> (8 * nb);
+    consumed += nb;
+    w += 4;
+  }
+}
+
+// ------------------------------------------------------------------ ValueMemory access
+// region words: stack frame 0 = words 0..31 (len 256), ctx = words 32..34 (len 24)
+XE_DEV void vmem_region(uint32_t h, int& wb, int64_t& len) {
+  if (xe_h_cls(h) == XE_H_CTX) { wb = XE_CTX_WORD0; len = XE_CTX_LEN; }
+  else { wb = 0; len = 256; }
+}
+
+XE_DEV int vmem_byte(const XeLane& L, int wb, int64_t off) {
+  uint64_t word = bm_word(L, wb + int(off >> 3));
+  return int((word >> (8 * (off & 7))) & 0xffu);
+}
+
+// ValueMemory.Read, memory.go:32-53 -> object id
+XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id) {
+  int wb; int64_t len;
+  vmem_region(h, wb, len);
+  if (int e = bounds(off, size, len)) return e;
+  int first = vmem_byte(L, wb, off);
+  for (int i = 1; i < size; i++)
+    if (vmem_byte(L, wb, off + i) != first) return XE_E_NONCONTIG;
+  if (!first) return XE_E_UNINIT;
+  id = first;
+  return 0;
+}
+
+XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
+  int64_t end = off + size;
+  int w0 = int(off >> 3), w1 = int((end - 1) >> 3);
+  for (int w = w0; w <= w1; w++) {
+    int64_t lo = off > int64_t(w) * 8 ? off - int64_t(w) * 8 : 0;
+    int64_t hi = end < int64_t(w + 1) * 8 ? end - int64_t(w) * 8 : 8;
+    uint64_t mask = (hi - lo == 8) ? ~0ull : (((1ull << (8 * (hi - lo))) - 1ull) << (8 * lo));
+    uint64_t word = bm_word(L, wb + w);
+    word = (word & ~mask) | ((uint64_t(id) * 0x0101010101010101ull) & mask);
+    bm_set_word(L, wb + w, word);
+  }
+}
+
+// ------------------------------------------------------------------ generic memory ops
+// Memory.Read for either kind. Outputs the RegisterValue to put in a register.
+XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size, bool track,
+                    uint32_t& kind, uint32_t& oh, int64_t& val, uint32_t& alias) {
+  uint32_t c = xe_h_cls(h);
+  if (c == XE_H_CTX || c == XE_H_STACK) {
+    int id = 0;
+    if (int e = vmem_read(L, h, off, size, id)) return e;
+    uint32_t t;
+    obj_get(L, id, val, oh, t);
+    kind = XE_T_KIND(t);
+    alias = (uint32_t(id) << 8) | (t & XE_T_RO);
+    return 0;
+  }
+  XeBMem B;
+  bmem_resolve(L, P, h, B);
+  if (int e = bounds(off, size, B.len)) return e;
+  if (B.map && track) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, size));
+  val = int64_t(load_le(B.base + off, size));
+  kind = XE_KIND_IMM;
+  oh = 0;
+  alias = 0;
+  return 0;
+}
+
+// Memory.Write of a new object {kind, oh, val} (ST: new IMM; STX: Copy of src)
+XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size,
+                     uint32_t kind, uint32_t oh, int64_t val) {
+  uint32_t c = xe_h_cls(h);
+  if (c == XE_H_CTX || c == XE_H_STACK) {
+    int wb; int64_t len;
+    vmem_region(h, wb, len);
+    if (int e = bounds(off, size, len)) return e;
+    int id = obj_alloc(L);
+    if (id < 0) return XE_EV_CAP;
+    obj_set(L, id, val, oh, kind);
+    vmem_fill(L, wb, off, size, id);
+    return 0;
+  }
+  XeBMem B;
+  bmem_resolve(L, P, h, B);
+  if (int e = bounds(off, size, B.len)) return e;
+  if (B.map && P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // non-commutative shared write
+  store_le(B.base + off, size, uint64_t(val));
+  return 0;
+}
+
+// PointerValue.ReadRange (registers.go:218-220,273-281; memory.go:55-95,176-185).
+// emit(i, byte) receives the output bytes. Returns 0 / XE_E_OOB / panic. dry = validate only.
+template <class Emit>
+XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Emit emit) {
+  uint32_t kind = XE_T_KIND(L.rt[r]);
+  uint32_t h = L.rh[r];
+  int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, L.rv[r]) : L.rv[r];
+  uint32_t c = xe_h_cls(h);
+  if (c == XE_H_CTX || c == XE_H_STACK) {
+    int wb; int64_t len;
+    vmem_region(h, wb, len);
+    if (off < 0 || xe_wadd(off, count) > len) return XE_E_OOB;
+    if (off >= len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
+    for (int64_t i = 0; i < count;) {
+      int v = vmem_byte(L, wb, off + i);
+      if (!v) { emit(i, 0); i++; continue; }
+      int size = 1;
+      for (int64_t j = i + 1; j < i + 8 && j < count; j++) {
+        if (vmem_byte(L, wb, off + j) != v) break;
+        size++;
+      }
+      int w = size > 4 ? 8 : size > 2 ? 4 : size > 1 ? 2 : 1;
+      if (i + w > count) return XE_EV_PANIC | XE_P_INDEX;
+      int64_t ov; uint32_t oh, ot;
+      obj_get(L, v, ov, oh, ot);
+      for (int b = 0; b < w; b++) emit(i + b, uint8_t(uint64_t(ov) >> (8 * b)));
+      i += w;
+    }
+    return 0;
+  }
+  XeBMem B;
+  bmem_resolve(L, P, h, B);
+  if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
+  if (B.map && count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
+  for (int64_t i = 0; i < count; i++) emit(i, B.base[off + i]);
+  return 0;
+}
+
+// ------------------------------------------------------------------ hash map
+XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
+  if (empty) return (M.state[M.cap] & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
+  uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
+  uint32_t mask = M.cap - 1;
+  uint32_t idx = uint32_t(hv) & mask;
+  for (uint32_t probe = 0; probe < M.cap; probe++) {
+    uint32_t st = M.state[idx];
+    if (!(st & XE_SLOT_FULL)) return -1;
+    const uint64_t* k = M.keys + uint64_t(idx) * M.kwords;
+    bool eq = true;
+    for (uint32_t w = 0; w < M.kwords; w++) eq = eq && (k[w] == kw[w]);
+    if (eq) return int64_t(idx);
+    idx = (idx + 1) & mask;
+  }
+  return -1;
+}
+
+// insert a new key (sequential mode only); returns slot
+XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty) {
+  if (empty) {
+    M.state[M.cap] = XE_SLOT_FULL;
+    *M.count += 1;
+    return int64_t(M.cap);
+  }
+  uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
+  uint32_t mask = M.cap - 1;
+  uint32_t idx = uint32_t(hv) & mask;
+  while (M.state[idx] & XE_SLOT_FULL) idx = (idx + 1) & mask;
+  uint64_t* k = M.keys + uint64_t(idx) * M.kwords;
+  for (uint32_t w = 0; w < M.kwords; w++) k[w] = kw[w];
+  M.state[idx] = XE_SLOT_FULL;
+  *M.count += 1;
+  return int64_t(idx);
+}
+
+// read a key through a pointer register into zero-padded words; ReadRange errors give the nil key
+// (maps_hash.go:50-53). Returns a panic code or 0.
+XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint64_t* kw, bool& empty) {
+  for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
+  int e = ptr_read_range(L, P, r, int64_t(M.key_size), [&](int64_t i, uint8_t b) {
+    kw[i >> 3] |= uint64_t(b) << (8 * (i & 7));
+  });
+  if (XE_IS_PANIC(e)) return e;
+  empty = e != 0 || M.key_size == 0;
+  if (empty)
+    for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
+  return 0;
+}
+
+// ------------------------------------------------------------------ helpers
+// regToMap, helper_functions.go:109-130. m = 0 means "R0 := 0, helper returns nil".
+XE_DEV int reg_to_map(XeLane& L, const XeParams& P, uint32_t& m) {
+  int64_t idx = L.rv[1];
+  if (XE_T_KIND(L.rt[1]) == XE_KIND_MEMPTR) {
+    uint32_t k, oh, al; int64_t v;
+    if (int e = mem_read(L, P, L.rh[1], L.rv[1], 4, true, k, oh, v, al)) return e;
+    idx = v;
+  }
+  if (idx < 1 || idx > int64_t(P.nmaps)) {
+    reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
+    m = 0;
+    return 0;
+  }
+  m = uint32_t(idx);
+  return 0;
+}
+
+XE_DEV int helper_errno_result(XeLane& L, int64_t v) {
+  reg_replace(L, 0, XE_KIND_IMM, 0, v, 0);
+  return 0;
+}
+
+// MapLookupElement, helper_functions.go:46-73
+XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
+  uint32_t m;
+  if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (!m) return 0;
+  const XeDevMap& M = P.maps[m];
+  if (XE_T_KIND(L.rt[2]) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
+  if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
+    uint32_t kind = XE_T_KIND(L.rt[2]);
+    int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, L.rv[2]) : L.rv[2];
+    uint32_t k, oh, al; int64_t kv;
+    int e = mem_read(L, P, L.rh[2], off, 4, true, k, oh, kv, al);
+    if (XE_IS_PANIC(e)) return e;
+    if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;  // error ignored, nil keyValReg.Value()
+    int64_t voff = xe_wmul(kv, int64_t(M.value_size));
+    if (voff >= int64_t(M.vals_bytes)) reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
+    else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), voff, 0);
+    return 0;
+  }
+  if (M.kind == XE_DM_HASH) {  // HashMap.Lookup, maps_hash.go:44-63
+    uint64_t kw[XE_MAX_KEY / 8];
+    bool empty = false;
+    if (int e = read_key(L, P, 2, M, kw, empty)) return e;
+    int64_t slot = hash_find(M, kw, empty);
+    if (slot < 0) reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
+    else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), 0, 0);
+    return 0;
+  }
+  return XE_EV_UNSUP;
+}
+
+// MapUpdateElement, helper_functions.go:76-101
+XE_DEV int helper_update(XeLane& L, const XeParams& P) {
+  uint32_t m;
+  if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (!m) return 0;
+  const XeDevMap& M = P.maps[m];
+  if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
+    if (XE_T_KIND(L.rt[3]) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
+    if (XE_T_KIND(L.rt[2]) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
+    uint32_t k, oh, al; int64_t kv;
+    if (int e = mem_read(L, P, L.rh[2], L.rv[2], 4, true, k, oh, kv, al))
+      return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+    if (kv >= int64_t(M.vals_bytes)) return helper_errno_result(L, -7);
+    for (int64_t i = 0; i < int64_t(M.value_size); i++) {
+      int64_t v;
+      if (int e = mem_read(L, P, L.rh[3], i, 1, true, k, oh, v, al))  // ignores the value ptr offset
+        return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+      int64_t dst = xe_wadd(xe_wmul(kv, int64_t(M.value_size)), i);
+      if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+      M.vals[dst] = uint8_t(v);
+    }
+    return helper_errno_result(L, 0);
+  }
+  if (M.kind == XE_DM_HASH) {  // HashMap.Update, maps_hash.go:65-123
+    if (XE_T_KIND(L.rt[2]) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    uint64_t kw[XE_MAX_KEY / 8];
+    bool empty = false;
+    if (int e = read_key(L, P, 2, M, kw, empty)) return e;
+    int64_t slot = hash_find(M, kw, empty);
+    if (slot < 0 && uint64_t(*M.count) + 1 > M.max_entries) return helper_errno_result(L, -7);
+    if (XE_T_KIND(L.rt[3]) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    // value ReadRange: validate first (a panic must leave the map untouched)
+    int ve = ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t, uint8_t) {});
+    if (XE_IS_PANIC(ve)) return ve;
+    if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+    if (slot < 0) slot = hash_insert_new(M, kw, empty);
+    uint8_t* dst = M.vals + uint64_t(slot) * M.value_size;
+    if (ve) {
+      M.state[slot] |= XE_SLOT_VLEN0;  // nil backing
+    } else {
+      M.state[slot] &= ~XE_SLOT_VLEN0;
+      ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; });
+    }
+    return helper_errno_result(L, 0);
+  }
+  return XE_EV_UNSUP;
+}
+
+XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn) {
+  if (fn >= 192) return XE_E_NO_HELPER;
+  if (fn < 0) return XE_EV_PANIC | XE_P_INDEX;
+  switch (fn) {
+    case 1: return helper_lookup(L, P);
+    case 2: return helper_update(L, P);
+    case 3: return XE_E_NOT_IMPL | XE_E_IN_HELPER;
+    case 14: reg_replace(L, 0, XE_KIND_IMM, 0, (int64_t(1234) << 32) + 5678, 0); return 0;
+    case 12: case 25: case 87: case 88: case 89: return XE_EV_UNSUP;
+  }
+  return XE_E_NO_HELPER;
+}
+
+// ------------------------------------------------------------------ ALU
+XE_DEV int shift_check(int64_t s) { return s < 0 ? (XE_EV_PANIC | XE_P_NEG_SHIFT) : 0; }
+
+XE_DEV int alu_compute(uint32_t op, bool wide, int64_t d, int64_t s, int64_t& out) {
+  if (!wide) {
+    int32_t a = xe_i32(d), b = xe_i32(s);
+    switch (op) {
+      case 0x00: out = int64_t(int32_t(uint32_t(a) + uint32_t(b))); return 0;
+      case 0x10: out = int64_t(int32_t(uint32_t(a) - uint32_t(b))); return 0;
+      case 0x20: out = int64_t(int32_t(uint32_t(a) * uint32_t(b))); return 0;
+      case 0x50: out = int64_t(a & b); return 0;
+      case 0x40: out = int64_t(a | b); return 0;
+      case 0xa0: out = int64_t(a ^ b); return 0;
+      case 0x30:
+        if (b == 0) return XE_EV_PANIC | XE_P_DIV0;
+        out = b == -1 ? int64_t(int32_t(0u - uint32_t(a))) : int64_t(a / b);
+        return 0;
+      case 0x90:
+        if (b == 0) return XE_EV_PANIC | XE_P_DIV0;
+        out = b == -1 ? 0 : int64_t(a % b);
+        return 0;
+      case 0x60: if (int e = shift_check(b)) return e; out = b >= 32 ? 0 : int64_t(uint32_t(uint32_t(d) << b)); return 0;
+      case 0x70: if (int e = shift_check(b)) return e; out = b >= 32 ? 0 : int64_t(uint32_t(d) >> b); return 0;
+      case 0xc0: if (int e = shift_check(b)) return e; out = int64_t(b >= 32 ? (a < 0 ? -1 : 0) : (a >> b)); return 0;
+    }
+  } else {
+    switch (op) {
+      case 0x00: out = xe_wadd(d, s); return 0;
+      case 0x10: out = int64_t(uint64_t(d) - uint64_t(s)); return 0;
+      case 0x20: out = xe_wmul(d, s); return 0;
+      case 0x50: out = d & s; return 0;
+      case 0x40: out = d | s; return 0;
+      case 0xa0: out = d ^ s; return 0;
+      case 0x30:
+        if (s == 0) return XE_EV_PANIC | XE_P_DIV0;
+        out = s == -1 ? int64_t(0ull - uint64_t(d)) : d / s;
+        return 0;
+      case 0x90:
+        if (s == 0) return XE_EV_PANIC | XE_P_DIV0;
+        out = s == -1 ? 0 : d % s;
+        return 0;
+      case 0x60: if (int e = shift_check(s)) return e; out = s >= 64 ? 0 : int64_t(uint64_t(d) << s); return 0;
+      case 0x70: if (int e = shift_check(s)) return e; out = s >= 64 ? 0 : int64_t(uint64_t(d) >> s); return 0;
+      case 0xc0: if (int e = shift_check(s)) return e; out = s >= 64 ? (d < 0 ? -1 : 0) : (d >> s); return 0;
+    }
+  }
+  out = 0;
+  return 0;
+}
+
+XE_DEV bool jmp_cond(uint32_t op, bool wide, int64_t d, int64_t s) {
+  if (!wide) {
+    int32_t a = xe_i32(d), b = xe_i32(s);
+    uint32_t ua = uint32_t(a), ub = uint32_t(b);
+    switch (op) {
+      case 0x10: return a == b;
+      case 0x50: return a != b;
+      case 0x20: return ua > ub;
+      case 0x30: return ua >= ub;
+      case 0x60: return a > b;
+      case 0x70: return a >= b;
+      case 0xc0: return a <= b;  // JSLT as written (inst_jslt.go:24,77)
+      case 0xd0: return a <= b;
+    }
+  } else {
+    switch (op) {
+      case 0x10: return d == s;
+      case 0x50: return d != s;
+      case 0x20: return uint64_t(d) > uint64_t(s);
+      case 0x30: return uint64_t(d) >= uint64_t(s);
+      case 0x60: return d > s;
+      case 0x70: return d >= s;
+      case 0xc0: return d <= s;  // inst_jslt.go:48,106
+      case 0xd0: return d <= s;
+    }
+  }
+  return false;
+}
+
+// effective offset of a pointer register + insn offset (inst_load.go:91-101)
+XE_DEV int64_t ptr_eff(const XeLane& L, int r, int32_t ioff) {
+  return XE_T_KIND(L.rt[r]) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(256, L.rv[r]), ioff)
+                                                 : xe_wadd(L.rv[r], ioff);
+}
+
+// ------------------------------------------------------------------ one instruction
+// Executes uop u (at pc) on this lane. Returns 0 (continue; `tgt` = PC after the instruction,
+// before Step's increment), XE_EV_EXIT, or an error code.
+XE_DEV int exec_uop(XeLane& L, const XeParams& P, const XeUop& u, int32_t pc, int32_t& tgt) {
+  tgt = pc;
+  const int d = u.dst, s = u.src;
+  switch (u.cls) {
+    case U_FAIL: return u.imm;
+    case U_NOP: return 0;
+    case U_EXIT: return XE_EV_EXIT;
+    case U_JA: tgt = u.tgt; return 0;
+    case U_ALU: {
+      bool wide = u.fl & UF_WIDE, reg = u.fl & UF_REG;
+      int64_t dv = L.rv[d];
+      int64_t sv = reg ? L.rv[s] : int64_t(u.imm);
+      if (reg && u.x == 0x00 && XE_T_KIND(L.rt[s]) != XE_KIND_IMM) {
+        // inst_add.go:82-98,131-147: dst becomes a Copy of the pointer src with the sum as offset
+        int64_t v = wide ? xe_wadd(dv, sv) : int64_t(int32_t(uint32_t(xe_i32(dv)) + uint32_t(xe_i32(sv))));
+        reg_replace(L, d, XE_T_KIND(L.rt[s]), L.rh[s], v, 0);
+        return 0;
+      }
+      if ((u.x == 0x30 || u.x == 0x90) && sv == 0) return XE_E_DIV0;
+      int64_t v;
+      if (int e = alu_compute(u.x, wide, dv, sv, v)) return e;
+      return reg_inplace(L, d, v);
+    }
+    case U_MOVI: reg_replace(L, d, XE_KIND_IMM, 0, int64_t(u.imm), 0); return 0;
+    case U_MOVR: reg_replace(L, d, XE_T_KIND(L.rt[s]), L.rh[s], L.rv[s], 0); return 0;
+    case U_NEG: {
+      int64_t dv = L.rv[d];
+      int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(xe_i32(dv))));
+      return reg_inplace(L, d, v);
+    }
+    case U_END: {
+      uint64_t rv = uint64_t(L.rv[d]), v;
+      if (u.x == 0) {
+        v = u.imm == 16 ? uint64_t(__builtin_bswap16(uint16_t(rv)))
+          : u.imm == 32 ? uint64_t(__builtin_bswap32(uint32_t(rv))) : __builtin_bswap64(rv);
+      } else {
+        v = u.imm == 16 ? uint64_t(uint16_t(rv)) : u.imm == 32 ? uint64_t(uint32_t(rv)) : rv;
+      }
+      return reg_inplace(L, d, int64_t(v));
+    }
+    case U_JMP: {
+      bool wide = u.fl & UF_WIDE;
+      int64_t dv = L.rv[d];
+      bool taken;
+      if (u.fl & UF_REG) {
+        bool same = XE_T_KIND(L.rt[d]) == XE_T_KIND(L.rt[s]);
+        bool c = jmp_cond(u.x, wide, dv, L.rv[s]);
+        taken = u.x == 0x50 ? (!same || c) : (same && c);
+      } else {
+        bool imm = XE_T_KIND(L.rt[d]) == XE_KIND_IMM;
+        bool c = jmp_cond(u.x, wide, dv, int64_t(u.imm));
+        taken = u.x == 0x50 ? (!imm || c) : (imm && c);
+      }
+      if (taken) tgt = u.tgt;
+      return 0;
+    }
+    case U_LDIMM64: {
+      if (s == 1) { reg_replace(L, d, XE_KIND_IMM, 0, int64_t(uint32_t(u.imm)), 0); return 0; }
+      if (s == 2) {  // BPF_PSEUDO_MAP_FD_VALUE, inst_load.go:36-63
+        uint32_t m = uint32_t(u.imm);
+        if (uint64_t(m) >= uint64_t(P.nmaps) + 1) return XE_E_NO_MAP;
+        if (m == 0) return XE_EV_PANIC | XE_P_NIL_MAP;
+        const XeDevMap& M = P.maps[m];
+        if (M.kind == XE_DM_ARRAY) {
+          if (M.vals_bytes == 0) return XE_E_MAP_NOT_PTR;
+          reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), int64_t(u.x), 0);
+          return 0;
+        }
+        if (M.kind == XE_DM_HASH) {
+          uint64_t kw[XE_MAX_KEY / 8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          bool empty = M.key_size > 4 || M.key_size == 0;  // ReadRange of a 4-byte tmp memory
+          int64_t slot = hash_find(M, kw, empty);
+          if (slot < 0) return XE_E_MAP_NOT_PTR;
+          reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), int64_t(u.x), 0);
+          return 0;
+        }
+        return XE_EV_UNSUP;
+      }
+      return reg_inplace(L, d, int64_t((uint64_t(u.x) << 32) + uint64_t(uint32_t(u.imm))));
+    }
+    case U_LDX: {
+      if (XE_T_KIND(L.rt[s]) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
+      int64_t off = ptr_eff(L, s, u.tgt);
+      uint32_t kind, oh, al; int64_t v;
+      if (int e = mem_read(L, P, L.rh[s], off, uop_size(u), true, kind, oh, v, al)) return e;
+      if (u.fl & UF_BADDST) return XE_E_ASSIGN_REG;
+      reg_replace(L, d, kind, oh, v, al);
+      return 0;
+    }
+    case U_ST: {
+      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+      return mem_write(L, P, L.rh[d], ptr_eff(L, d, u.tgt), uop_size(u), XE_KIND_IMM, 0, int64_t(u.imm));
+    }
+    case U_STX: {
+      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+      return mem_write(L, P, L.rh[d], ptr_eff(L, d, u.tgt), uop_size(u), XE_T_KIND(L.rt[s]), L.rh[s], L.rv[s]);
+    }
+    case U_ATOMIC: {
+      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+      uint32_t h = L.rh[d];
+      int64_t off = ptr_eff(L, d, u.tgt);
+      int size = uop_size(u);
+      uint32_t c = xe_h_cls(h);
+      if (c == XE_H_CTX || c == XE_H_STACK) {
+        int id = 0;
+        if (int e = vmem_read(L, h, off, size, id)) return e;
+        if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+        int64_t ov; uint32_t oh, ot;
+        obj_get(L, id, ov, oh, ot);
+        if (XE_T_KIND(ot) == XE_KIND_FRAMEPTR && (ot & XE_T_RO)) return XE_E_READONLY;
+        int64_t nv = xe_wadd(ov, L.rv[s]);
+        obj_set_val(L, id, nv);
+#pragma unroll
+        for (int j = 0; j < 10; j++)
+          if (XE_T_ALIAS(L.rt[j]) == uint32_t(id)) L.rv[j] = nv;
+        return 0;
+      }
+      XeBMem B;
+      bmem_resolve(L, P, h, B);
+      if (int e = bounds(off, size, B.len)) return e;
+      if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+      if (B.map) {
+        fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
+        atomic_add_field(B.base + off, size, uint64_t(L.rv[s]));
+      } else {
+        uint64_t cur = load_le(B.base + off, size);
+        store_le(B.base + off, size, cur + uint64_t(L.rv[s]));
+      }
+      return 0;
+    }
+    case U_HELPER: return call_helper(L, P, int64_t(u.imm));
+    case U_CALLX: return call_helper(L, P, L.rv[d]);
+    case U_CALLBPF: return XE_EV_UNSUP;
+  }
+  return XE_EV_UNSUP;
+}
+
+// ------------------------------------------------------------------ wave driver
+// minimum of v over the wave (all lanes active)
+XE_DEV int wave_min(int v) {
+  int cur = xe_readfirst(v);
+  unsigned long long lt = xe_ballot(v < cur);
+  while (lt) {
+    int l = __builtin_ctzll(lt);
+    cur = xe_readlane(v, l);
+    lt = xe_ballot(v < cur);
+  }
+  return cur;
+}
+
+// Runs the per-packet harness for packet index `i` on this lane (valid=false:
+// the lane idles). All lanes of the wave must call this together.
+XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+  // ---- Reset (emulator/vm.go:211-246) + harness ctx
+  for (int r = 0; r < 10; r++) reg_replace(L, r, XE_KIND_IMM, 0, 0, 0);
+  reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
+  reg_replace(L, 1, XE_KIND_MEMPTR, xe_h_make(XE_H_CTX, 0, 0), 0, 0);
+  L.dirty = 0;
+  L.oused = 0x7full;
+  L.odef = 0x7eull;
+  L.pkt = P.umem;
+  L.plen = 0;
+  if (valid) {
+    xe_desc dsc = P.desc[i];
+    uint64_t a = dsc.addr, l = dsc.len;
+    if (a > P.umem_len || l > P.umem_len - a) l = 0;
+    L.pkt = P.umem + a;
+    L.plen = int64_t(l);
+  }
+  // ingress / rx queue objects are IMMs with settings values: materialise them eagerly
+  obj_set(L, 4, int64_t(P.ingress), 0, XE_KIND_IMM);
+  obj_set(L, 5, int64_t(P.rxq), 0, XE_KIND_IMM);
+
+  int status = valid ? -1 : XE_ST_OK;  // -1 = running
+  int code = 0;
+  int32_t pc = 0, res_pc = 0;
+  uint64_t steps = 0;
+
+  for (;;) {
+    int mypc = status == -1 ? pc : 0x7fffffff;
+    int sel = wave_min(mypc);
+    if (sel == 0x7fffffff) break;
+    if (status == -1 && pc == sel) {
+      if (steps >= P.max_steps) {
+        status = XE_ST_BUDGET; res_pc = pc;
+      } else if (sel < 0 || sel >= P.prog_len) {
+        status = XE_ST_PANIC; code = XE_P_INDEX; res_pc = pc;  // program[PC] (vm.go:143)
+      } else {
+        const XeUop u = P.prog[sel];  // wave-uniform: scalar load
+        steps++;
+        int32_t tgt;
+        int e = exec_uop(L, P, u, sel, tgt);
+        res_pc = sel;
+        if (e == 0) {
+          if (int64_t(P.prog_len) <= int64_t(tgt) + 1) {  // vm.go:162-167
+            status = XE_ST_VMERR; code = XE_E_BAD_PC;
+          } else {
+            pc = tgt + 1;
+          }
+        } else if (e == XE_EV_EXIT) {
+          status = XE_ST_OK;
+        } else if (XE_EV_CLASS(e) == XE_EV_ORD) {
+          status = XE_ST_INTERNAL_ORDERED;
+        } else if (XE_EV_CLASS(e) == XE_EV_CAP) {
+          status = XE_ST_CAPACITY;
+        } else if (XE_EV_CLASS(e) == XE_EV_UNSUP) {
+          status = XE_ST_UNSUPPORTED;
+        } else if (XE_IS_PANIC(e)) {
+          status = XE_ST_PANIC; code = e & 0xff;
+        } else {
+          status = XE_ST_VMERR; code = e & 0xffff;
+        }
+      }
+    }
+  }
+
+  if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
+  if (status == XE_ST_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
+  if (valid) {
+    if (P.results) {
+      xe_result r;
+      r.status = uint8_t(status);
+      r.r0_kind = uint8_t(XE_T_KIND(L.rt[0]));
+      r.code = uint16_t(code);
+      r.pc = uint32_t(res_pc);
+      r.r0 = L.rv[0];
+      P.results[i] = r;
+    }
+    if (P.verdicts) P.verdicts[i] = uint32_t(uint64_t(L.rv[0]));
+    if (P.regs) {
+      xe_regs g;
+      for (int r = 0; r < 10; r++) {
+        g.val[r] = L.rv[r];
+        uint32_t k = XE_T_KIND(L.rt[r]);
+        g.kind[r] = uint8_t(k);
+        if (k == XE_KIND_IMM) { g.region[r] = 0xff; g.map[r] = 0; }
+        else {
+          uint32_t c = xe_h_cls(L.rh[r]);
+          g.region[r] = uint8_t(c);
+          g.map[r] = uint8_t((c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(L.rh[r]) : 0);
+        }
+      }
+      g.pad[0] = g.pad[1] = 0;
+      g.steps = uint32_t(steps);
+      P.regs[i] = g;
+    }
+  }
+  // batch statistics: one atomic per wave per counter
+  unsigned long long my_steps = valid ? steps : 0;
+#if defined(__HIPCC__)
+  for (int o = 32; o > 0; o >>= 1) my_steps += __shfl_xor(my_steps, o);
+#endif
+  if (xe_lane() == 0 && my_steps) xe_atomic_add64(&P.stats[0], my_steps);
+  for (int st = 0; st < 8; st++) {
+    unsigned long long c = __builtin_popcountll(xe_ballot(valid && status == st));
+    if (c && xe_lane() == 0) xe_atomic_add64(&P.stats[1 + st], c);
+  }
+}
+
+// flush per-lane footprints of maps 1..4 to global (wave OR-reduction, one atomic per word)
+XE_DEV void flush_footprints(XeLane& L, const XeParams& P) {
+  for (int k = 0; k < 4; k++) {
+    if (uint32_t(k + 1) > P.nmaps) break;
+    unsigned long long r = L.fpr[k], a = L.fpa[k];
+#if defined(__HIPCC__)
+    for (int o = 32; o > 0; o >>= 1) { r |= __shfl_xor(r, o); a |= __shfl_xor(a, o); }
+#endif
+    if (xe_lane() == 0) {
+      if (r) xe_atomic_or64(&P.fp[(k + 1) * 2], r);
+      if (a) xe_atomic_or64(&P.fp[(k + 1) * 2 + 1], a);
+    }
+  }
+}

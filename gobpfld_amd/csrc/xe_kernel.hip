@@ -1,0 +1,61 @@
+// xe_kernel.hip — gfx950 kernels of the batched eBPF/XDP emulator.
+//
+// xe_interp_kernel: one lane per packet (wave64), grid-stride over 64-packet chunks in parallel
+// mode; a single lane walking the packets in order in sequential mode (exact fallback for
+// order-dependent map effects). xe_delta_kernel / xe_apply_delta_kernel: u64 counter deltas for
+// the multi-GPU all-reduce.
+#include "xe_interp.h"
+
+extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
+  XeLane L;
+#pragma unroll
+  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  const int lane = xe_lane();
+  if (P.mode == XE_MODE_SEQUENTIAL) {
+    if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+    for (uint32_t i = 0; i < P.n; i++) run_packet(L, P, i, lane == 0);
+  } else {
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nchunks = (P.n + 63u) >> 6;
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+      // a lane elsewhere needed an ordered write: this run will be discarded, stop early
+      if (__builtin_amdgcn_readfirstlane(xe_load_relaxed32(P.flags)) & XE_FLAG_ORDERED) break;
+      const uint32_t i = c * 64u + uint32_t(lane);
+      run_packet(L, P, i, i < P.n);
+    }
+  }
+  flush_footprints(L, P);
+}
+
+extern "C" __global__ void xe_delta_kernel(const unsigned long long* cur, const unsigned long long* snap,
+                                           unsigned long long* out, uint64_t nwords) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x)
+    out[i] = cur[i] - snap[i];
+}
+
+extern "C" __global__ void xe_apply_delta_kernel(unsigned long long* cur, const unsigned long long* snap,
+                                                 const unsigned long long* delta, uint64_t nwords) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x)
+    cur[i] = snap[i] + delta[i];
+}
+
+// host-side launchers (called from xe_runtime.cpp)
+extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
+  hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), 0, s, *P);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s) {
+  uint32_t blocks = uint32_t(nwords / 256 + 1);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(xe_delta_kernel, dim3(blocks), dim3(256), 0, s, (const unsigned long long*)cur,
+                     (const unsigned long long*)snap, (unsigned long long*)out, nwords);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s) {
+  uint32_t blocks = uint32_t(nwords / 256 + 1);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(xe_apply_delta_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)cur,
+                     (const unsigned long long*)snap, (const unsigned long long*)delta, nwords);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,833 @@
+// xe_runtime.cpp — host runtime and C ABI (include/xdpemu.h) of the batched eBPF/XDP emulator.
+//
+// * decoder + translator: raw eBPF -> 16-byte micro-ops, reproducing ebpf.Decode's accept/reject
+//   table (ebpf/decode.go:8-917) and emulator.Translate's (emulator/inst.go:21-238); register-number
+//   errors that the reference would raise deterministically at run time become U_FAIL micro-ops.
+// * maps: ARRAY and HASH realised as device-resident tables (host mirror for userspace access).
+// * batch runs: parallel kernel, footprint/ordered-write verification, exact sequential fallback.
+//
+// Built twice: with hipcc into gobpfld_amd/libxdpemu.so (the product), and with g++ -DXE_HOSTSIM
+// into tests/hostsim/ (CPU-only test build of the same logic; never loaded by the product).
+#include "xe_internal.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#ifdef XE_HOSTSIM
+#include "xe_interp.h"
+typedef void* xe_stream_t;
+#else
+#include <hip/hip_runtime_api.h>
+typedef hipStream_t xe_stream_t;
+extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
+extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
+#endif
+
+namespace {
+
+// ------------------------------------------------------------------ backend
+#ifdef XE_HOSTSIM
+int dev_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
+void dev_free(void* p) { free(p); }
+int h2d(void* d, const void* h, size_t n, xe_stream_t) { memcpy(d, h, n); return 0; }
+int d2h(void* h, const void* d, size_t n, xe_stream_t) { memcpy(h, d, n); return 0; }
+int d2d(void* d, const void* s, size_t n, xe_stream_t) { memmove(d, s, n); return 0; }
+int dmemset(void* d, int v, size_t n, xe_stream_t) { memset(d, v, n); return 0; }
+int dsync(xe_stream_t) { return 0; }
+int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
+  XeLane L;
+  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  for (uint32_t i = 0; i < P->n; i++) {
+    if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
+    run_packet(L, *P, i, true);
+  }
+  flush_footprints(L, *P);
+  return 0;
+}
+int launch_delta(const void* cur, const void* snap, void* out, uint64_t nw, xe_stream_t) {
+  for (uint64_t i = 0; i < nw; i++) ((uint64_t*)out)[i] = ((const uint64_t*)cur)[i] - ((const uint64_t*)snap)[i];
+  return 0;
+}
+int launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nw, xe_stream_t) {
+  for (uint64_t i = 0; i < nw; i++) ((uint64_t*)cur)[i] = ((const uint64_t*)snap)[i] + ((const uint64_t*)delta)[i];
+  return 0;
+}
+struct Timer {
+  std::chrono::steady_clock::time_point t;
+  void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
+  static float ms(const Timer& a, const Timer& b) { return std::chrono::duration<float, std::milli>(b.t - a.t).count(); }
+  void init() {}
+  void fini() {}
+};
+int set_device(int) { return 0; }
+#else
+int dev_alloc(void** p, size_t n) { return hipMalloc(p, n ? n : 8) == hipSuccess ? 0 : -1; }
+void dev_free(void* p) { if (p) (void)hipFree(p); }
+int h2d(void* d, const void* h, size_t n, xe_stream_t s) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1; }
+int d2h(void* h, const void* d, size_t n, xe_stream_t s) { return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) == hipSuccess ? 0 : -1; }
+int d2d(void* d, const void* src, size_t n, xe_stream_t s) { return hipMemcpyAsync(d, src, n, hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1; }
+int dmemset(void* d, int v, size_t n, xe_stream_t s) { return hipMemsetAsync(d, v, n, s) == hipSuccess ? 0 : -1; }
+int dsync(xe_stream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -1; }
+int launch_interp(const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_launch_interp(P, b, t, s); }
+int launch_delta(const void* c, const void* sn, void* o, uint64_t nw, xe_stream_t s) { return xe_launch_delta(c, sn, o, nw, s); }
+int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t nw, xe_stream_t s) { return xe_launch_apply_delta(c, sn, d, nw, s); }
+struct Timer {
+  hipEvent_t e = nullptr;
+  void init() { if (!e) (void)hipEventCreate(&e); }
+  void fini() { if (e) (void)hipEventDestroy(e); e = nullptr; }
+  void rec(xe_stream_t s) { init(); (void)hipEventRecord(e, s); }
+  static float ms(const Timer& a, const Timer& b) { float m = 0; (void)hipEventElapsedTime(&m, a.e, b.e); return m; }
+};
+int set_device(int d) { return hipSetDevice(d) == hipSuccess ? 0 : -1; }
+#endif
+
+// ------------------------------------------------------------------ decoder + translator
+int size_log2(uint8_t sizecode) {  // ebpf.Size: W=0x00, H=0x08, B=0x10, DW=0x18 (ebpf/ebpf.go:106-116)
+  switch (sizecode) { case 0x00: return 2; case 0x08: return 1; case 0x10: return 0; default: return 3; }
+}
+
+XeUop fail_uop(int code) { XeUop u{}; u.cls = U_FAIL; u.imm = code; return u; }
+
+// Returns XE_OK, XE_ERR_DECODE or XE_ERR_TRANSLATE.
+int translate(const uint64_t* raw, uint32_t n, std::vector<XeUop>& out, std::string& err) {
+  out.assign(n, XeUop{});
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t r = raw[i];
+    const uint8_t op = uint8_t(r);
+    const uint8_t dst = uint8_t(r >> 8) & 0x0f, src = uint8_t(r >> 12) & 0x0f;
+    const int16_t off = int16_t(uint16_t(r >> 16));
+    const int32_t imm = int32_t(uint32_t(r >> 32));
+    const uint8_t cls = op & 7;
+    XeUop u{};
+    bool decoded = true, translated = true;
+
+    if (op == 0x18) {  // LD_IMM64 (ebpf/decode.go:21-36) + its Nop filler slot
+      if (i + 1 >= n) { err = "decode: load double word imm op code found but not enough instructions"; return XE_ERR_DECODE; }
+      if (dst > 9) u = fail_uop(XE_E_BAD_REG);  // Registers.Get(dst) first, inst_load.go:22-25
+      else { u.cls = U_LDIMM64; u.dst = dst; u.src = src; u.imm = imm; u.x = uint32_t(raw[i + 1] >> 32); }
+      out[i] = u;
+      out[i + 1] = XeUop{}; out[i + 1].cls = U_NOP;
+      i++;
+      continue;
+    }
+    switch (op) {
+      case 0x20: case 0x28: case 0x30: case 0x38:  // LD ABS / IND: translate, fail at run time
+      case 0x40: case 0x48: case 0x50: case 0x58:
+        u = fail_uop(XE_E_NOT_IMPL);
+        break;
+      case 0x61: case 0x69: case 0x71: case 0x79:  // LDX (inst_load.go:84-118)
+        if (src > 10) { u = fail_uop(XE_E_BAD_REG); break; }
+        u.cls = U_LDX; u.src = src; u.tgt = off; u.fl = uint8_t(size_log2(op ^ 0x61) << 4);
+        if (dst > 9) u.fl |= UF_BADDST; else u.dst = dst;
+        break;
+      case 0x62: case 0x6a: case 0x72: case 0x7a:  // ST (inst_store.go:20-51)
+        if (dst > 10) { u = fail_uop(XE_E_BAD_REG); break; }
+        u.cls = U_ST; u.dst = dst; u.imm = imm; u.tgt = off; u.fl = uint8_t(size_log2(op ^ 0x62) << 4);
+        break;
+      case 0x63: case 0x6b: case 0x73: case 0x7b:  // STX (inst_store.go:64-99)
+        if (src > 9 || dst > 10) { u = fail_uop(XE_E_BAD_REG); break; }
+        u.cls = U_STX; u.dst = dst; u.src = src; u.tgt = off; u.fl = uint8_t(size_log2(op ^ 0x63) << 4);
+        break;
+      case 0xc3: case 0xcb: case 0xd3: case 0xdb: {  // atomics (decode.go:124-184)
+        bool known = imm == 0x00 || imm == 0x01 || imm == 0x10 || imm == 0x11 || imm == 0x50 || imm == 0x51 ||
+                     imm == 0x40 || imm == 0x41 || imm == 0xa0 || imm == 0xa1 || imm == 0xe1 || imm == 0xf1;
+        if (!known) { decoded = false; break; }
+        if (imm != 0x00 && imm != 0x01) { translated = false; break; }  // only AtomicAdd (inst.go:52-53)
+        if (dst > 10) { u = fail_uop(XE_E_BAD_REG); break; }
+        u.cls = U_ATOMIC; u.dst = dst; u.tgt = off; u.fl = uint8_t(size_log2(op ^ 0xc3) << 4);
+        if (src > 9) u.fl |= UF_BADSRC; else u.src = src;
+        break;
+      }
+      default:
+        if (cls == 0x04 || cls == 0x07) {  // ALU / ALU64 (decode.go:186-540)
+          const uint8_t aop = op & 0xf0;
+          const bool x = op & 0x08, wide = cls == 0x07;
+          if (aop == 0x80) {  // NEG: K form only
+            if (x) { decoded = false; break; }
+            if (dst > 9) { u = fail_uop(XE_E_BAD_REG); break; }
+            u.cls = U_NEG; u.dst = dst; u.fl = wide ? UF_WIDE : 0;
+          } else if (aop == 0xd0) {  // END: ALU class, imm 16/32/64
+            if (wide || !(imm == 16 || imm == 32 || imm == 64)) { decoded = false; break; }
+            if (dst > 9) { u = fail_uop(XE_E_BAD_REG); break; }
+            u.cls = U_END; u.dst = dst; u.imm = imm; u.x = x ? 8 : 0;
+          } else if (aop == 0xe0 || aop == 0xf0) {
+            decoded = false;
+          } else if (aop == 0xb0) {  // MOV (inst_mov.go)
+            if (!x) {
+              if (dst > 9) { u = fail_uop(XE_E_ASSIGN_REG); break; }
+              u.cls = U_MOVI; u.dst = dst; u.imm = imm;
+            } else {
+              if (src > 10) { u = fail_uop(XE_E_BAD_REG); break; }
+              if (dst > 9) { u = fail_uop(XE_E_ASSIGN_REG); break; }
+              u.cls = U_MOVR; u.dst = dst; u.src = src;
+            }
+            u.fl = wide ? UF_WIDE : 0;
+          } else {
+            if (dst > 9 || (x && src > 9)) { u = fail_uop(XE_E_BAD_REG); break; }
+            u.cls = U_ALU; u.dst = dst; u.src = x ? src : 0; u.imm = imm; u.x = aop;
+            u.fl = uint8_t((wide ? UF_WIDE : 0) | (x ? UF_REG : 0));
+          }
+        } else if (cls == 0x05 || cls == 0x06) {  // JMP / JMP32 (decode.go:544-902)
+          const uint8_t jop = op & 0xf0;
+          const bool x = op & 0x08;
+          if (op == 0x05) { u.cls = U_JA; u.tgt = int32_t(i) + off; break; }
+          if (op == 0x85) {
+            if (src == 1) { u.cls = U_CALLBPF; u.imm = imm; }  // ebpf.PSEUDO_CALL
+            else { u.cls = U_HELPER; u.imm = imm; }
+            break;
+          }
+          if (op == 0x8d) {  // CALLX: helper id in register Register(imm) (uint8 truncation)
+            uint8_t reg = uint8_t(imm);
+            if (reg > 9) { u = fail_uop(XE_E_BAD_REG); break; }
+            u.cls = U_CALLX; u.dst = reg;
+            break;
+          }
+          if (op == 0x95) { u.cls = U_EXIT; break; }
+          switch (jop) {
+            case 0x10: case 0x20: case 0x30: case 0x50: case 0x60: case 0x70: case 0xc0: case 0xd0:
+              if (dst > 9 || (x && src > 9)) { u = fail_uop(XE_E_BAD_REG); break; }
+              u.cls = U_JMP; u.dst = dst; u.src = x ? src : 0; u.imm = imm; u.x = jop;
+              u.tgt = int32_t(i) + off;
+              u.fl = uint8_t((cls == 0x05 ? UF_WIDE : 0) | (x ? UF_REG : 0));
+              break;
+            case 0x40: case 0xa0: case 0xb0: translated = false; break;  // JSET / JLT / JLE
+            default: decoded = false;
+          }
+        } else {
+          decoded = false;
+        }
+    }
+    if (!decoded) {
+      char b[200];
+      snprintf(b, sizeof b, "decode: unable to decode raw instruction, inst: %u, op: %2x, imm: %8x", i, op, uint32_t(imm));
+      err = b;
+      return XE_ERR_DECODE;
+    }
+    if (!translated) {
+      char b[200];
+      snprintf(b, sizeof b, "add program: translate: can't translate instruction at %u (op %2x)", i, op);
+      err = b;
+      // the reference decodes the whole program before translating (vm.go:61-73): finish decoding
+      std::vector<XeUop> rest;
+      std::string e2;
+      if (i + 1 < n) {
+        int rc = translate(raw + i + 1, n - i - 1, rest, e2);
+        if (rc == XE_ERR_DECODE) { err = e2; return XE_ERR_DECODE; }
+      }
+      return XE_ERR_TRANSLATE;
+    }
+    out[i] = u;
+  }
+  return XE_OK;
+}
+
+// ------------------------------------------------------------------ maps
+uint32_t next_pow2(uint64_t v) {
+  uint32_t p = 16;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+struct HostMap {
+  xe_map_def def{};
+  uint32_t dkind = XE_DM_NONE;
+  uint32_t cap = 0, kwords = 0;
+  uint64_t vals_bytes = 0, vals_alloc = 0;
+  std::vector<uint8_t> vals;
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> state;
+  uint32_t count = 0;
+  uint8_t* d_vals = nullptr;
+  uint64_t* d_keys = nullptr;
+  uint32_t* d_state = nullptr;
+  uint32_t* d_count = nullptr;
+  uint8_t* d_snap = nullptr;
+  bool host_dirty = true, dev_dirty = false;
+
+  uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
+  void pack_key(const void* key, uint64_t* kw) const {
+    for (uint32_t w = 0; w < kwords; w++) kw[w] = 0;
+    memcpy(kw, key, def.key_size);
+  }
+  int64_t find(const uint64_t* kw) {
+    if (def.key_size == 0) return (state[cap] & XE_SLOT_FULL) ? int64_t(cap) : -1;
+    uint32_t idx = uint32_t(xe_hash_words(kw, kwords, def.key_size)) & (cap - 1);
+    for (uint32_t p = 0; p < cap; p++) {
+      if (!(state[idx] & XE_SLOT_FULL)) return -1;
+      if (!memcmp(key_at(idx), kw, kwords * 8)) return idx;
+      idx = (idx + 1) & (cap - 1);
+    }
+    return -1;
+  }
+  int64_t insert(const uint64_t* kw) {
+    if (def.key_size == 0) { state[cap] = XE_SLOT_FULL; count++; return cap; }
+    uint32_t idx = uint32_t(xe_hash_words(kw, kwords, def.key_size)) & (cap - 1);
+    while (state[idx] & XE_SLOT_FULL) idx = (idx + 1) & (cap - 1);
+    memcpy(key_at(idx), kw, kwords * 8);
+    state[idx] = XE_SLOT_FULL;
+    count++;
+    return idx;
+  }
+  // linear-probing delete with backward shift (keeps probe chains intact without tombstones)
+  void erase_slot(uint32_t i) {
+    const uint32_t mask = cap - 1;
+    if (i == cap) { state[cap] = 0; count--; return; }
+    state[i] = 0;
+    count--;
+    uint32_t j = i;
+    for (;;) {
+      j = (j + 1) & mask;
+      if (!(state[j] & XE_SLOT_FULL)) break;
+      uint32_t k = uint32_t(xe_hash_words(key_at(j), kwords, def.key_size)) & mask;
+      bool move = (j > i) ? (k <= i || k > j) : (k <= i && k > j);
+      if (move) {
+        memcpy(key_at(i), key_at(j), kwords * 8);
+        memcpy(vals.data() + uint64_t(i) * def.value_size, vals.data() + uint64_t(j) * def.value_size, def.value_size);
+        state[i] = state[j];
+        state[j] = 0;
+        i = j;
+      }
+    }
+  }
+};
+
+}  // namespace
+
+struct xe_vm {
+  xe_settings settings{};
+  std::vector<std::vector<XeUop>> programs{std::vector<XeUop>()};  // index 0 invalid
+  int32_t entry = 0;
+  std::vector<HostMap> maps{HostMap()};                              // index 0 invalid
+  std::string last_error;
+  xe_stream_t stream = nullptr;
+  // device buffers
+  XeUop* d_prog = nullptr;
+  int32_t d_prog_idx = -1;
+  size_t d_prog_len = 0;
+  XeDevMap* d_maps = nullptr;
+  size_t d_maps_n = 0;
+  unsigned long long* d_aux = nullptr;  // [0..15] stats, [16] flags, [32..] footprints
+  // host-run staging
+  void* d_umem = nullptr; size_t d_umem_cap = 0;
+  void* d_desc = nullptr; size_t d_desc_cap = 0;
+  void* d_res = nullptr; size_t d_res_cap = 0;
+  void* d_ver = nullptr; size_t d_ver_cap = 0;
+  void* d_regs = nullptr; size_t d_regs_cap = 0;
+  std::vector<unsigned long long> last_fp;
+  uint32_t last_flags = 0;
+  Timer t0, t1, t2;
+};
+
+namespace {
+
+constexpr size_t kAuxWords = 32 + 2 * 64;
+
+int fail(xe_vm* vm, int rc, const std::string& msg) {
+  if (vm) vm->last_error = msg;
+  return rc;
+}
+
+int ensure_buf(void** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  dev_free(*p);
+  *p = nullptr;
+  size_t c = std::max<size_t>(need, 256);
+  if (dev_alloc(p, c)) { *cap = 0; return -1; }
+  *cap = c;
+  return 0;
+}
+
+int map_alloc_device(HostMap& m) {
+  if (dev_alloc((void**)&m.d_vals, m.vals_alloc)) return -1;
+  if (dev_alloc((void**)&m.d_snap, m.vals_alloc)) return -1;
+  if (m.dkind == XE_DM_HASH) {
+    if (dev_alloc((void**)&m.d_keys, std::max<size_t>(size_t(m.cap + 1) * m.kwords * 8, 8))) return -1;
+    if (dev_alloc((void**)&m.d_state, size_t(m.cap + 1) * 4)) return -1;
+    if (dev_alloc((void**)&m.d_count, 8)) return -1;
+  }
+  return 0;
+}
+
+void map_free_device(HostMap& m) {
+  dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count);
+  m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr;
+}
+
+int map_upload(xe_vm* vm, HostMap& m) {
+  if (h2d(m.d_vals, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
+  if (m.dkind == XE_DM_HASH) {
+    if (m.kwords && h2d(m.d_keys, m.keys.data(), size_t(m.cap + 1) * m.kwords * 8, vm->stream)) return -1;
+    if (h2d(m.d_state, m.state.data(), size_t(m.cap + 1) * 4, vm->stream)) return -1;
+    if (h2d(m.d_count, &m.count, 4, vm->stream)) return -1;
+  }
+  if (dsync(vm->stream)) return -1;
+  m.host_dirty = false;
+  return 0;
+}
+
+int map_download(xe_vm* vm, HostMap& m) {
+  if (!m.dev_dirty) return 0;
+  if (d2h(m.vals.data(), m.d_vals, m.vals_alloc, vm->stream)) return -1;
+  if (m.dkind == XE_DM_HASH) {
+    if (m.kwords && d2h(m.keys.data(), m.d_keys, size_t(m.cap + 1) * m.kwords * 8, vm->stream)) return -1;
+    if (d2h(m.state.data(), m.d_state, size_t(m.cap + 1) * 4, vm->stream)) return -1;
+    if (d2h(&m.count, m.d_count, 4, vm->stream)) return -1;
+  }
+  if (dsync(vm->stream)) return -1;
+  m.dev_dirty = false;
+  return 0;
+}
+
+HostMap* get_map(xe_vm* vm, int32_t idx) {
+  if (!vm || idx < 1 || idx >= int32_t(vm->maps.size())) return nullptr;
+  return &vm->maps[idx];
+}
+
+int prepare_run(xe_vm* vm) {
+  if (vm->entry < 1 || vm->entry >= int32_t(vm->programs.size()))
+    return fail(vm, XE_ERR_INVAL, "no program loaded at PI");
+  if (set_device(vm->settings.device)) return fail(vm, XE_ERR_DEVICE, "hipSetDevice failed");
+  const auto& prog = vm->programs[vm->entry];
+  if (vm->d_prog_idx != vm->entry) {
+    dev_free(vm->d_prog);
+    vm->d_prog = nullptr;
+    if (dev_alloc((void**)&vm->d_prog, std::max<size_t>(prog.size(), 1) * sizeof(XeUop)))
+      return fail(vm, XE_ERR_DEVICE, "device alloc (program)");
+    if (!prog.empty() && h2d(vm->d_prog, prog.data(), prog.size() * sizeof(XeUop), vm->stream))
+      return fail(vm, XE_ERR_DEVICE, "program upload");
+    vm->d_prog_idx = vm->entry;
+    vm->d_prog_len = prog.size();
+  }
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (m.host_dirty && map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+  }
+  std::vector<XeDevMap> dm(vm->maps.size());
+  memset(dm.data(), 0, dm.size() * sizeof(XeDevMap));
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    XeDevMap& d = dm[i];
+    d.kind = m.dkind;
+    d.key_size = m.def.key_size;
+    d.value_size = m.def.value_size;
+    d.max_entries = m.def.max_entries;
+    d.vals_bytes = m.vals_bytes;
+    d.vals = m.d_vals;
+    d.keys = m.d_keys;
+    d.state = m.d_state;
+    d.count = m.d_count;
+    d.cap = m.cap;
+    d.kwords = m.kwords;
+  }
+  if (vm->d_maps_n < dm.size()) {
+    dev_free(vm->d_maps);
+    vm->d_maps = nullptr;
+    if (dev_alloc((void**)&vm->d_maps, dm.size() * sizeof(XeDevMap))) return fail(vm, XE_ERR_DEVICE, "device alloc (maps)");
+    vm->d_maps_n = dm.size();
+  }
+  if (h2d(vm->d_maps, dm.data(), dm.size() * sizeof(XeDevMap), vm->stream)) return fail(vm, XE_ERR_DEVICE, "map table upload");
+  if (!vm->d_aux && dev_alloc((void**)&vm->d_aux, kAuxWords * 8)) return fail(vm, XE_ERR_DEVICE, "device alloc (aux)");
+  return XE_OK;
+}
+
+uint32_t grid_blocks(uint32_t n) {
+  uint64_t chunks = (uint64_t(n) + 63) / 64;
+  uint64_t blocks = (chunks + 3) / 4;  // 4 waves per 256-thread block
+  const uint64_t maxb = 256ull * 16;   // grid-stride beyond this
+  return uint32_t(std::max<uint64_t>(1, std::min(blocks, maxb)));
+}
+
+}  // namespace
+
+extern "C" {
+
+int xe_default_settings(xe_settings* s) {
+  if (!s) return XE_ERR_INVAL;
+  memset(s, 0, sizeof *s);
+  s->stack_frame_size = 256;
+  s->max_stack_frames = 8;
+  s->max_steps = 1u << 20;
+  s->ingress_ifindex = 1;
+  s->rx_queue_index = 0;
+  s->device = 0;
+  s->mode = XE_MODE_AUTO;
+  return XE_OK;
+}
+
+int xe_create(const xe_settings* s, xe_vm** out) {
+  if (!out) return XE_ERR_INVAL;
+  xe_vm* vm = new xe_vm();
+  if (s) vm->settings = *s;
+  else xe_default_settings(&vm->settings);
+  if (vm->settings.stack_frame_size == 0) vm->settings.stack_frame_size = 256;
+  if (vm->settings.max_stack_frames == 0) vm->settings.max_stack_frames = 8;
+  if (vm->settings.max_steps == 0) vm->settings.max_steps = 1u << 20;
+  if (vm->settings.stack_frame_size != 256 || vm->settings.max_stack_frames != 8) {
+    delete vm;
+    return XE_ERR_UNSUPPORTED;  // the device frame layout is fixed to DefaultVMSettings
+  }
+  if (set_device(vm->settings.device)) { delete vm; return XE_ERR_DEVICE; }
+#ifndef XE_HOSTSIM
+  if (hipStreamCreateWithFlags(&vm->stream, hipStreamNonBlocking) != hipSuccess) { delete vm; return XE_ERR_DEVICE; }
+#endif
+  *out = vm;
+  return XE_OK;
+}
+
+void xe_destroy(xe_vm* vm) {
+  if (!vm) return;
+  set_device(vm->settings.device);
+  for (auto& m : vm->maps) map_free_device(m);
+  dev_free(vm->d_prog); dev_free(vm->d_maps); dev_free(vm->d_aux);
+  dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
+  vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
+#ifndef XE_HOSTSIM
+  if (vm->stream) (void)hipStreamDestroy(vm->stream);
+#endif
+  delete vm;
+}
+
+const char* xe_last_error(const xe_vm* vm) { return vm ? vm->last_error.c_str() : "null vm"; }
+
+int xe_add_raw_program(xe_vm* vm, const uint64_t* insns, uint32_t n, int32_t* idx) {
+  if (!vm || (!insns && n)) return XE_ERR_INVAL;
+  std::vector<XeUop> prog;
+  std::string err;
+  int rc = translate(insns, n, prog, err);
+  if (rc) return fail(vm, rc, err);
+  vm->programs.push_back(std::move(prog));
+  if (idx) *idx = int32_t(vm->programs.size() - 1);
+  return XE_OK;
+}
+
+int xe_set_entrypoint(xe_vm* vm, int32_t idx) {  // emulator/vm.go:100-108
+  if (!vm) return XE_ERR_INVAL;
+  if (idx < 1 || int32_t(vm->programs.size()) <= idx) return fail(vm, XE_ERR_INVAL, "program index out of bounds");
+  vm->entry = idx;
+  return XE_OK;
+}
+
+int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_len, int32_t* idx) {
+  if (!vm || !def) return XE_ERR_INVAL;
+  if (vm->maps.size() > XE_H_MAX_MAPS) return fail(vm, XE_ERR_UNSUPPORTED, "at most 63 maps");
+  HostMap m;
+  m.def = *def;
+  switch (def->type) {  // AbstractMapToVM, emulator/maps.go:92-155
+    case XE_MAP_ARRAY: case XE_MAP_PERCPU_ARRAY: case XE_MAP_PROG_ARRAY: case XE_MAP_ARRAY_OF_MAPS:
+      m.dkind = XE_DM_ARRAY;
+      m.vals_bytes = uint64_t(def->value_size) * def->max_entries;
+      break;
+    case XE_MAP_HASH: case XE_MAP_PERCPU_HASH: case XE_MAP_HASH_OF_MAPS:
+      if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
+      m.dkind = XE_DM_HASH;
+      m.cap = next_pow2(uint64_t(def->max_entries) * 2);
+      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 2M)");
+      m.kwords = (def->key_size + 7) / 8;
+      m.vals_bytes = uint64_t(m.cap + 1) * def->value_size;
+      m.keys.assign(size_t(m.cap + 1) * m.kwords, 0);
+      m.state.assign(size_t(m.cap) + 1, 0);
+      break;
+    default:
+      return fail(vm, XE_ERR_MAPTYPE, "map type not yet implemented on the device");
+  }
+  m.vals_alloc = std::max<uint64_t>(8, (m.vals_bytes + 7) & ~uint64_t(7));
+  m.vals.assign(m.vals_alloc, 0);
+  if (init && (def->type == XE_MAP_ARRAY || def->type == XE_MAP_PERCPU_ARRAY))
+    memcpy(m.vals.data(), init, std::min<uint64_t>(init_len, m.vals_bytes));
+  if (set_device(vm->settings.device) || map_alloc_device(m)) {
+    map_free_device(m);
+    return fail(vm, XE_ERR_DEVICE, "device alloc (map)");
+  }
+  m.host_dirty = true;
+  vm->maps.push_back(std::move(m));
+  if (idx) *idx = int32_t(vm->maps.size() - 1);
+  return XE_OK;
+}
+
+int xe_map_lookup(xe_vm* vm, int32_t mi, const void* key, void* value) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !key) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_ARRAY) {
+    uint32_t kv; memcpy(&kv, key, 4);
+    if (kv >= m->def.max_entries) return 0;
+    if (value) memcpy(value, m->vals.data() + uint64_t(kv) * m->def.value_size, m->def.value_size);
+    return 1;
+  }
+  uint64_t kw[XE_MAX_KEY / 8];
+  m->pack_key(key, kw);
+  int64_t s = m->find(kw);
+  if (s < 0) return 0;
+  if (value) {
+    memset(value, 0, m->def.value_size);
+    if (!(m->state[s] & XE_SLOT_VLEN0)) memcpy(value, m->vals.data() + uint64_t(s) * m->def.value_size, m->def.value_size);
+  }
+  return 1;
+}
+
+int xe_map_update(xe_vm* vm, int32_t mi, const void* key, const void* value) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !key || !value) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_ARRAY) {
+    uint32_t kv; memcpy(&kv, key, 4);
+    if (kv >= m->def.max_entries) return fail(vm, XE_ERR_INVAL, "key out of range");
+    memcpy(m->vals.data() + uint64_t(kv) * m->def.value_size, value, m->def.value_size);
+  } else {
+    uint64_t kw[XE_MAX_KEY / 8];
+    m->pack_key(key, kw);
+    int64_t s = m->find(kw);
+    if (s < 0) {
+      if (uint64_t(m->count) + 1 > m->def.max_entries) return fail(vm, XE_ERR_NOMEM, "map is full");
+      s = m->insert(kw);
+    }
+    m->state[s] &= ~XE_SLOT_VLEN0;
+    memcpy(m->vals.data() + uint64_t(s) * m->def.value_size, value, m->def.value_size);
+  }
+  m->host_dirty = true;
+  return XE_OK;
+}
+
+int xe_map_delete(xe_vm* vm, int32_t mi, const void* key) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !key || m->dkind != XE_DM_HASH) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  uint64_t kw[XE_MAX_KEY / 8];
+  m->pack_key(key, kw);
+  int64_t s = m->find(kw);
+  if (s >= 0) {
+    memset(m->vals.data() + uint64_t(s) * m->def.value_size, 0, m->def.value_size);
+    m->erase_slot(uint32_t(s));
+    m->host_dirty = true;
+  }
+  return XE_OK;
+}
+
+int xe_map_count(xe_vm* vm, int32_t mi, uint64_t* count) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !count) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  *count = m->dkind == XE_DM_ARRAY ? m->def.max_entries : m->count;
+  return XE_OK;
+}
+
+int xe_map_dump(xe_vm* vm, int32_t mi, void* keys_or_raw, void* values, uint64_t cap, uint64_t* count) {
+  HostMap* m = get_map(vm, mi);
+  if (!m) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_ARRAY) {
+    if (count) *count = m->def.max_entries;
+    if (keys_or_raw && cap >= m->def.max_entries) memcpy(keys_or_raw, m->vals.data(), m->vals_bytes);
+    return XE_OK;
+  }
+  if (count) *count = m->count;
+  if (!keys_or_raw && !values) return XE_OK;
+  if (cap < m->count) return fail(vm, XE_ERR_INVAL, "dump buffer too small");
+  const uint32_t ks = m->def.key_size, vs = m->def.value_size;
+  std::vector<uint32_t> slots;
+  slots.reserve(m->count);
+  for (uint32_t s = 0; s <= m->cap; s++)
+    if (m->state[s] & XE_SLOT_FULL) slots.push_back(s);
+  auto keyp = [&](uint32_t s) -> const uint8_t* { return reinterpret_cast<const uint8_t*>(m->key_at(s)); };
+  // MA6: sorted by key bytes; the nil/empty key (slot cap) sorts first
+  std::sort(slots.begin(), slots.end(), [&](uint32_t a, uint32_t b) {
+    if (a == m->cap || b == m->cap) return a == m->cap && b != m->cap;
+    return memcmp(keyp(a), keyp(b), ks) < 0;
+  });
+  for (size_t i = 0; i < slots.size(); i++) {
+    uint32_t s = slots[i];
+    if (keys_or_raw) {
+      uint8_t* kd = (uint8_t*)keys_or_raw + i * ks;
+      if (s == m->cap) memset(kd, 0, ks); else memcpy(kd, keyp(s), ks);
+    }
+    if (values) {
+      uint8_t* vd = (uint8_t*)values + i * vs;
+      if (m->state[s] & XE_SLOT_VLEN0) memset(vd, 0, vs);
+      else memcpy(vd, m->vals.data() + uint64_t(s) * vs, vs);
+    }
+  }
+  return XE_OK;
+}
+
+int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
+                        void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
+  if (!vm) return XE_ERR_INVAL;
+  if (stats) memset(stats, 0, sizeof *stats);
+  if (int rc = prepare_run(vm)) return rc;
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
+
+  XeParams P{};
+  P.prog = vm->d_prog;
+  P.prog_len = int32_t(vm->d_prog_len);
+  P.umem = (uint8_t*)d_umem;
+  P.umem_len = umem_len;
+  P.desc = (const xe_desc*)d_desc;
+  P.n = n;
+  P.nmaps = uint32_t(vm->maps.size() - 1);
+  P.results = (xe_result*)d_results;
+  P.verdicts = (uint32_t*)d_verdicts;
+  P.regs = (xe_regs*)d_regs;
+  P.maps = vm->d_maps;
+  P.max_steps = vm->settings.max_steps;
+  P.ingress = vm->settings.ingress_ifindex;
+  P.rxq = vm->settings.rx_queue_index;
+  P.stats = vm->d_aux;
+  P.flags = reinterpret_cast<uint32_t*>(vm->d_aux + 16);
+  P.fp = vm->d_aux + 32;
+
+  const uint32_t mode = vm->settings.mode;
+  // snapshot map values: rollback point for the ordered fallback and base of the shard deltas
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (d2d(m.d_snap, m.d_vals, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "snapshot");
+  }
+  if (dmemset(vm->d_aux, 0, kAuxWords * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
+  vm->t0.rec(s);
+  bool conflict = false;
+  uint32_t used = XE_MODE_PARALLEL;
+  if (mode == XE_MODE_SEQUENTIAL) {
+    P.mode = XE_MODE_SEQUENTIAL;
+    used = XE_MODE_SEQUENTIAL;
+    if (launch_interp(&P, 1, 64, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+  } else {
+    P.mode = XE_MODE_PARALLEL;
+    if (launch_interp(&P, grid_blocks(n), 256, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+  }
+  vm->t1.rec(s);
+  std::vector<unsigned long long> aux(kAuxWords);
+  if (d2h(aux.data(), vm->d_aux, kAuxWords * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+  float kms = Timer::ms(vm->t0, vm->t1);
+  if (mode != XE_MODE_SEQUENTIAL) {
+    uint32_t flags = uint32_t(aux[16]);
+    conflict = (flags & XE_FLAG_ORDERED) != 0;
+    for (uint32_t m = 1; m <= P.nmaps && m < 64; m++)
+      if (aux[32 + 2 * m] & aux[32 + 2 * m + 1]) conflict = true;
+    if (conflict && mode == XE_MODE_AUTO) {
+      // order-dependent batch: roll the maps back and replay it in packet order on one lane
+      for (size_t i = 1; i < vm->maps.size(); i++) {
+        HostMap& m = vm->maps[i];
+        if (d2d(m.d_vals, m.d_snap, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      }
+      if (dmemset(vm->d_aux, 0, kAuxWords * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
+      P.mode = XE_MODE_SEQUENTIAL;
+      used = XE_MODE_SEQUENTIAL;
+      vm->t1.rec(s);
+      if (launch_interp(&P, 1, 64, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+      vm->t2.rec(s);
+      if (d2h(aux.data(), vm->d_aux, kAuxWords * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+      kms += Timer::ms(vm->t1, vm->t2);
+    }
+  }
+  vm->last_flags = uint32_t(aux[16]);
+  vm->last_fp.assign(aux.begin() + 32, aux.end());
+  for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
+  if (stats) {
+    stats->packets = n;
+    stats->steps = aux[0];
+    for (int k = 0; k < 8; k++) stats->status_count[k] = aux[1 + k];
+    stats->mode_used = used;
+    stats->conflict = conflict ? 1 : 0;
+    stats->kernel_ms = kms;
+    stats->total_ms = kms;
+  }
+  return XE_OK;
+}
+
+int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* desc, uint32_t n,
+                      xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats) {
+  if (!vm) return XE_ERR_INVAL;
+  if (set_device(vm->settings.device)) return fail(vm, XE_ERR_DEVICE, "hipSetDevice failed");
+  xe_stream_t s = vm->stream;
+  if (ensure_buf(&vm->d_umem, &vm->d_umem_cap, umem_len) || ensure_buf(&vm->d_desc, &vm->d_desc_cap, size_t(n) * 16) ||
+      ensure_buf(&vm->d_res, &vm->d_res_cap, size_t(n) * sizeof(xe_result)) ||
+      ensure_buf(&vm->d_ver, &vm->d_ver_cap, size_t(n) * 4) ||
+      (regs && ensure_buf(&vm->d_regs, &vm->d_regs_cap, size_t(n) * sizeof(xe_regs))))
+    return fail(vm, XE_ERR_DEVICE, "device alloc (batch)");
+  Timer a, b;
+  a.rec(s);
+  if ((umem_len && h2d(vm->d_umem, umem, umem_len, s)) || (n && h2d(vm->d_desc, desc, size_t(n) * 16, s)))
+    return fail(vm, XE_ERR_DEVICE, "H2D");
+  int rc = xe_run_batch_device(vm, vm->d_umem, umem_len, vm->d_desc, n, results ? vm->d_res : nullptr,
+                               verdicts ? vm->d_ver : nullptr, regs ? vm->d_regs : nullptr, s, stats);
+  if (rc) return rc;
+  if ((results && d2h(results, vm->d_res, size_t(n) * sizeof(xe_result), s)) ||
+      (verdicts && d2h(verdicts, vm->d_ver, size_t(n) * 4, s)) ||
+      (regs && d2h(regs, vm->d_regs, size_t(n) * sizeof(xe_regs), s)) ||
+      (umem_len && d2h(umem, vm->d_umem, umem_len, s)))
+    return fail(vm, XE_ERR_DEVICE, "D2H");
+  b.rec(s);
+  if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
+  if (stats) stats->total_ms = Timer::ms(a, b);
+  a.fini(); b.fini();
+  return XE_OK;
+}
+
+int xe_map_values_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !bytes) return XE_ERR_INVAL;
+  *bytes = m->vals_alloc;
+  return XE_OK;
+}
+
+int xe_map_delta(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !d_out) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (launch_delta(m->d_vals, m->d_snap, d_out, m->vals_alloc / 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "delta");
+  return XE_OK;
+}
+
+int xe_map_apply_delta(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !d_in) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (launch_apply_delta(m->d_vals, m->d_snap, d_in, m->vals_alloc / 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "apply delta");
+  m->dev_dirty = true;
+  return XE_OK;
+}
+
+int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords) {
+  if (!vm) return XE_ERR_INVAL;
+  uint32_t nm = uint32_t(vm->maps.size());
+  uint32_t need = 1 + 2 * nm;
+  if (nwords) *nwords = need;
+  if (!out) return XE_OK;
+  if (cap_words < need) return XE_ERR_INVAL;
+  out[0] = vm->last_flags;
+  for (uint32_t i = 0; i < 2 * nm; i++) out[1 + i] = i < vm->last_fp.size() ? vm->last_fp[i] : 0;
+  return XE_OK;
+}
+
+const char* xe_version(void) {
+#ifdef XE_HOSTSIM
+  return "xdpemu-hostsim 0.1 (CPU test build of the device logic; not the product)";
+#else
+  return "xdpemu 0.1 gfx950";
+#endif
+}
+
+int xe_device_count(int* n) {
+  if (!n) return XE_ERR_INVAL;
+#ifdef XE_HOSTSIM
+  *n = 0;
+  return XE_OK;
+#else
+  return hipGetDeviceCount(n) == hipSuccess ? XE_OK : XE_ERR_DEVICE;
+#endif
+}
+
+}  // extern "C"

@@ -1,0 +1,202 @@
+"""Host-side mirror of gobpfld's `emulator` package API over the MI355X device emulator.
+
+    vm = VM(Settings())                      # emulator.NewVM            (emulator/vm.go:30-48)
+    prog = vm.add_raw_program(insns)         # VM.AddRawProgram          (emulator/vm.go:61-73)
+    m = vm.add_map(MapDef(...), initial)     # VM.AddMap/AddAbstractMap  (emulator/vm.go:75-98)
+    vm.set_entrypoint(prog)                  # VM.SetEntrypoint          (emulator/vm.go:100-108)
+    res = vm.run_batch(umem, descs)          # Reset + R1=ctx + Run per packet (vm.go:110-246)
+    vm.map_dump(m)                           # final map state (Map.Keys + Lookup)
+
+Errors raise EmulatorError carrying the library's message (the Go API returns `error`).
+Per-packet failures never raise: they are reported in the result's `status`.
+The product library is the HIP one; passing another `lib` is for tests only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+STATUS = {0: "OK", 1: "VMERR", 2: "PANIC", 3: "BUDGET", 4: "UNSUPPORTED", 5: "CAPACITY"}
+MAP_HASH, MAP_ARRAY, MAP_PROG_ARRAY, MAP_PERF_EVENT_ARRAY, MAP_PERCPU_HASH, MAP_PERCPU_ARRAY = 1, 2, 3, 4, 5, 6
+MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL = 0, 1, 2
+
+
+class EmulatorError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"{msg} (rc={rc})")
+        self.rc = rc
+
+
+@dataclass
+class MapDef:
+    type: int
+    key_size: int
+    value_size: int
+    max_entries: int
+    flags: int = 0
+
+
+@dataclass
+class Settings:
+    max_steps: int = 1 << 20
+    ingress_ifindex: int = 1
+    rx_queue_index: int = 0
+    device: int = 0
+    mode: int = MODE_AUTO
+
+
+@dataclass
+class BatchResult:
+    results: np.ndarray        # structured (status, r0_kind, code, pc, r0)
+    verdicts: np.ndarray       # uint32(R0)
+    regs: np.ndarray | None    # structured parity records or None
+    stats: dict
+
+
+def _stats_dict(s: N.BatchStats) -> dict:
+    return {"packets": s.packets, "steps": s.steps, "status_count": list(s.status_count),
+            "mode_used": s.mode_used, "conflict": s.conflict, "kernel_ms": s.kernel_ms,
+            "total_ms": s.total_ms}
+
+
+class VM:
+    def __init__(self, settings: Settings | None = None, lib: N.Lib | None = None):
+        self.lib = lib or N.product()
+        s = settings or Settings()
+        cs = N.Settings()
+        self.lib.default_settings(C.byref(cs)) if self.lib.has("default_settings") else None
+        cs.stack_frame_size, cs.max_stack_frames = 256, 8
+        cs.max_steps, cs.ingress_ifindex, cs.rx_queue_index = s.max_steps, s.ingress_ifindex, s.rx_queue_index
+        cs.device, cs.mode = s.device, s.mode
+        self.settings = s
+        h = C.c_void_p()
+        rc = self.lib.create(C.byref(cs), C.byref(h))
+        if rc:
+            raise EmulatorError(rc, "create VM")
+        self.h = h
+        self.map_defs: dict[int, MapDef] = {}
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc < 0:
+            raise EmulatorError(rc, f"{what}: {self.lib.last_error(self.h).decode(errors='replace')}")
+
+    # ---- programs / maps
+    def add_raw_program(self, insns) -> int:
+        arr = np.ascontiguousarray(np.asarray(insns, dtype=np.uint64))
+        idx = C.c_int32()
+        self._check(self.lib.add_raw_program(self.h, arr.ctypes.data, len(arr), C.byref(idx)), "add raw program")
+        return idx.value
+
+    def set_entrypoint(self, idx: int) -> None:
+        self._check(self.lib.set_entrypoint(self.h, idx), "set entrypoint")
+
+    def add_map(self, d: MapDef, initial: bytes | np.ndarray | None = None) -> int:
+        md = N.MapDef(d.type, d.key_size, d.value_size, d.max_entries, d.flags)
+        buf = None if initial is None else np.frombuffer(bytes(initial), dtype=np.uint8)
+        idx = C.c_int32()
+        self._check(self.lib.add_map(self.h, C.byref(md), None if buf is None else buf.ctypes.data,
+                                     0 if buf is None else len(buf), C.byref(idx)), "add map")
+        self.map_defs[idx.value] = d
+        return idx.value
+
+    def map_update(self, m: int, key: bytes, value: bytes) -> None:
+        d = self.map_defs[m]
+        k = bytes(key).ljust(max(d.key_size, 4), b"\0")
+        v = bytes(value).ljust(d.value_size, b"\0")
+        self._check(self.lib.map_update(self.h, m, k, v), "map update")
+
+    def map_lookup(self, m: int, key: bytes) -> bytes | None:
+        d = self.map_defs[m]
+        k = bytes(key).ljust(max(d.key_size, 4), b"\0")
+        out = C.create_string_buffer(max(d.value_size, 1))
+        rc = self.lib.map_lookup(self.h, m, k, out)
+        self._check(rc, "map lookup")
+        return out.raw[: d.value_size] if rc == 1 else None
+
+    def map_delete(self, m: int, key: bytes) -> None:
+        d = self.map_defs[m]
+        self._check(self.lib.map_delete(self.h, m, bytes(key).ljust(max(d.key_size, 4), b"\0")), "map delete")
+
+    def map_dump(self, m: int):
+        """ARRAY -> raw bytes (ValueSize*MaxEntries); HASH -> (keys[n,ks], values[n,vs]) sorted by key."""
+        d = self.map_defs[m]
+        cnt = C.c_uint64()
+        self._check(self.lib.map_dump(self.h, m, None, None, 0, C.byref(cnt)), "map dump")
+        n = cnt.value
+        if d.type in (MAP_ARRAY, MAP_PERCPU_ARRAY, MAP_PROG_ARRAY, 12):
+            raw = np.zeros(d.value_size * d.max_entries, dtype=np.uint8)
+            self._check(self.lib.map_dump(self.h, m, raw.ctypes.data, None, n, C.byref(cnt)), "map dump")
+            return raw.tobytes()
+        keys = np.zeros((n, d.key_size), dtype=np.uint8)
+        vals = np.zeros((n, d.value_size), dtype=np.uint8)
+        self._check(self.lib.map_dump(self.h, m, keys.ctypes.data if n else None,
+                                      vals.ctypes.data if n else None, n, C.byref(cnt)), "map dump")
+        return keys, vals
+
+    def map_values_bytes(self, m: int) -> int:
+        b = C.c_uint64()
+        self._check(self.lib.map_values_bytes(self.h, m, C.byref(b)), "map values bytes")
+        return b.value
+
+    # ---- running
+    def run_batch(self, umem: np.ndarray, descs: np.ndarray, want_regs: bool = False) -> BatchResult:
+        """Host-memory batch (end-to-end form). `umem` (uint8) receives packet writes."""
+        d_desc, d_res, d_regs = N.np_dtypes()
+        assert umem.dtype == np.uint8 and umem.flags.c_contiguous
+        descs = np.ascontiguousarray(descs, dtype=d_desc)
+        n = len(descs)
+        res = np.zeros(n, dtype=d_res)
+        ver = np.zeros(n, dtype=np.uint32)
+        regs = np.zeros(n, dtype=d_regs) if want_regs else None
+        st = N.BatchStats()
+        fn = self.lib.run_batch_host if self.lib.has("run_batch_host") else self.lib.run_batch
+        rc = fn(self.h, umem.ctypes.data if umem.size else None, umem.size, descs.ctypes.data if n else None, n,
+                res.ctypes.data if n else None, ver.ctypes.data if n else None,
+                regs.ctypes.data if (regs is not None and n) else None, C.byref(st))
+        self._check(rc, "run batch")
+        return BatchResult(res, ver, regs, _stats_dict(st))
+
+    def run_batch_device(self, d_umem: int, umem_len: int, d_desc: int, n: int, d_results: int = 0,
+                         d_verdicts: int = 0, d_regs: int = 0, stream: int = 0) -> dict:
+        """Device-resident batch: all pointers are device addresses (e.g. torch tensor .data_ptr())."""
+        st = N.BatchStats()
+        rc = self.lib.run_batch_device(self.h, d_umem or None, umem_len, d_desc or None, n, d_results or None,
+                                       d_verdicts or None, d_regs or None, stream or None, C.byref(st))
+        self._check(rc, "run batch (device)")
+        return _stats_dict(st)
+
+    # ---- multi-GPU shard support
+    def map_delta(self, m: int, d_out: int, stream: int = 0) -> None:
+        self._check(self.lib.map_delta(self.h, m, d_out, stream or None), "map delta")
+
+    def map_apply_delta(self, m: int, d_in: int, stream: int = 0) -> None:
+        self._check(self.lib.map_apply_delta(self.h, m, d_in, stream or None), "map apply delta")
+
+    def footprint(self) -> np.ndarray:
+        nw = C.c_uint32()
+        self._check(self.lib.footprint(self.h, None, 0, C.byref(nw)), "footprint")
+        out = np.zeros(nw.value, dtype=np.uint64)
+        self._check(self.lib.footprint(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), nw.value, C.byref(nw)),
+                    "footprint")
+        return out

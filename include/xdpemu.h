@@ -1,0 +1,223 @@
+/*
+ * xdpemu.h — C ABI of the MI355X-native batched eBPF/XDP emulator.
+ *
+ * Drop-in boundary for the userspace VM of dylandreimerink/gobpfld (`emulator/`).
+ * Every entry point names the reference interface it replaces (paths relative to the
+ * reference module root). The Go-side cgo binding a maintainer would add is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions:
+ *   - integer return codes: 0 = ok, negative = errno-like (XE_ERR_*); xe_last_error() has text;
+ *   - per-packet failures are reported in xe_result.status, never as a call failure;
+ *   - the library copies programs and map definitions;
+ *   - one xe_vm per host thread (the reference VM is not goroutine-safe either, emulator/vm.go:14-28).
+ *
+ * Plain pointers and sizes only: no torch or HIP types in the signatures. Device pointers are
+ * passed as `void*`/`const void*` and a HIP stream as `void*` (0 = the VM's own stream).
+ */
+#ifndef XDPEMU_H
+#define XDPEMU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- call return codes ---------------------------------------------------------------- */
+#define XE_OK 0
+#define XE_ERR_INVAL (-22)     /* bad argument / bad index (e.g. SetEntrypoint out of bounds) */
+#define XE_ERR_DECODE (-100)   /* ebpf.Decode rejected the program   (ebpf/decode.go:905-913) */
+#define XE_ERR_TRANSLATE (-101) /* emulator.Translate rejected it      (emulator/inst.go:230-231) */
+#define XE_ERR_MAPTYPE (-102)  /* AbstractMapToVM: type not implemented (emulator/maps.go:155) */
+#define XE_ERR_NOMEM (-12)
+#define XE_ERR_DEVICE (-200)   /* HIP runtime failure */
+#define XE_ERR_UNSUPPORTED (-95)
+
+/* ---- per-packet status (parity taxonomy) -------------------- */
+#define XE_ST_OK 0          /* top-level exit; verdict = R0 (emulator/inst_exit.go:24-26)          */
+#define XE_ST_VMERR 1       /* Run() returned a *VMError (emulator/vm.go:175-180)                  */
+#define XE_ST_PANIC 2       /* the Go VM would panic (runtime error not recovered anywhere)        */
+#define XE_ST_BUDGET 3      /* step budget exhausted (the Go VM has none and would hang)           */
+#define XE_ST_UNSUPPORTED 4 /* feature outside this build's scope (tail call, perf output, ...)    */
+#define XE_ST_CAPACITY 5    /* device per-lane object table overflowed (device-only; see DESIGN)   */
+
+/* VMERR codes (xe_result.code when status == XE_ST_VMERR). Errors raised inside a helper
+ * (emulator/inst_call_helper.go:30-33) carry XE_E_IN_HELPER in addition. */
+#define XE_E_NO_PROGRAM 1   /* emulator/vm.go:138-140 */
+#define XE_E_BAD_REG 2      /* Registers.Get/Copy unknown register, emulator/registers.go:88,115 */
+#define XE_E_ASSIGN_REG 3   /* Registers.Assign can't assign, emulator/registers.go:145 */
+#define XE_E_READONLY 4     /* FramePointer.Assign on a readonly pointer, emulator/registers.go:306-308 */
+#define XE_E_DIV0 5         /* emulator/inst_div.go:10, emulator/inst_mod.go:10 */
+#define XE_E_NONPTR_LOAD 6  /* emulator/inst_load.go:103-105 */
+#define XE_E_NONPTR_STORE 7 /* emulator/inst_store.go:41-43,89-91; emulator/inst_atomic.go:40-42 */
+#define XE_E_OOB 8          /* emulator/memory.go:33-35,56-58,98-100,136-138,177-179,188-190 */
+#define XE_E_NONCONTIG 9    /* emulator/memory.go:43-45 */
+#define XE_E_UNINIT 10      /* emulator/memory.go:48-50 */
+#define XE_E_BAD_PC 11      /* emulator/vm.go:114-115,162-167 */
+#define XE_E_NOT_IMPL 12    /* emulator/inst_load.go:131-148, helper 3 (helper_functions.go:104-106) */
+#define XE_E_NO_HELPER 13   /* emulator/inst_call_helper.go:21-28,55-63 */
+#define XE_E_NO_MAP 14      /* emulator/inst_load.go:39-41 */
+#define XE_E_MAP_NOT_PTR 15 /* emulator/inst_load.go:49-52 */
+#define XE_E_MAP_OP 16      /* map Lookup/Update returned an error the helper does not map to errno */
+#define XE_E_IN_HELPER 0x80
+
+/* PANIC codes (xe_result.code when status == XE_ST_PANIC) */
+#define XE_P_NIL_DEREF 1 /* nil interface method call, e.g. emulator/maps_array.go:72-75 */
+#define XE_P_NEG_SHIFT 2 /* Go shift by a negative count, emulator/inst_lsh.go:26 etc. */
+#define XE_P_DIV0 3      /* int32 divide by zero after a non-zero 64-bit check, emulator/inst_div.go:96 */
+#define XE_P_INDEX 4     /* index/slice out of range (negative PC, negative helper id, ReadRange) */
+#define XE_P_NIL_MAP 5   /* vm.Maps[0] == nil used as a map, emulator/inst_load.go:43-44 */
+
+/* register kinds (emulator/registers.go:176-324) */
+#define XE_KIND_IMM 0
+#define XE_KIND_MEMPTR 1
+#define XE_KIND_FRAMEPTR 2
+
+/* memory regions a pointer can refer to (parity records) */
+#define XE_REGION_PACKET 0
+#define XE_REGION_CTX 1
+#define XE_REGION_STACK 2
+#define XE_REGION_ARRAY 3
+#define XE_REGION_HASHVAL 4
+
+/* map types: numeric values of bpftypes.BPFMapType (bpftypes/bpf_types.go:155-277) */
+#define XE_MAP_HASH 1
+#define XE_MAP_ARRAY 2
+#define XE_MAP_PROG_ARRAY 3
+#define XE_MAP_PERF_EVENT_ARRAY 4
+#define XE_MAP_PERCPU_HASH 5
+#define XE_MAP_PERCPU_ARRAY 6
+#define XE_MAP_LRU_HASH 9
+#define XE_MAP_LRU_PERCPU_HASH 10
+#define XE_MAP_ARRAY_OF_MAPS 12
+#define XE_MAP_HASH_OF_MAPS 13
+#define XE_MAP_QUEUE 22
+#define XE_MAP_STACK 23
+
+/* run modes */
+#define XE_MODE_AUTO 0       /* parallel, verified; falls back to ordered device execution on conflict */
+#define XE_MODE_PARALLEL 1   /* parallel only; conflicts reported in stats, results kept            */
+#define XE_MODE_SEQUENTIAL 2 /* exact packet order on one device lane                             */
+
+/* AF_XDP descriptor, exactly the layout of gobpfld's xsk.go:695-701 */
+typedef struct xe_desc {
+    uint64_t addr;
+    uint32_t len;
+    uint32_t options;
+} xe_desc;
+
+/* per-packet result */
+typedef struct xe_result {
+    uint8_t status;  /* XE_ST_* */
+    uint8_t r0_kind; /* XE_KIND_* of R0 */
+    uint16_t code;   /* XE_E_* / XE_P_* */
+    uint32_t pc;     /* PC of the exiting / faulting instruction */
+    int64_t r0;      /* R0.Value() (emulator/registers.go:91-116) */
+} xe_result;
+
+/* optional parity record: R0..R9 after the run (VMError snapshot registers on error) */
+typedef struct xe_regs {
+    int64_t val[10];
+    uint8_t kind[10];
+    uint8_t region[10];  /* XE_REGION_* for pointers, 0xff for IMM */
+    uint8_t map[10];     /* map index for ARRAY/HASHVAL regions, else 0 */
+    uint8_t pad[2];
+    uint32_t steps;      /* instructions executed */
+} xe_regs;
+
+/* gobpfld.BPFMapDef (map_definition.go:15-27) */
+typedef struct xe_map_def {
+    uint32_t type;
+    uint32_t key_size;
+    uint32_t value_size;
+    uint32_t max_entries;
+    uint32_t flags;
+} xe_map_def;
+
+/* emulator.VMSettings (emulator/vm.go:282-296) plus the harness/device knobs */
+typedef struct xe_settings {
+    int32_t stack_frame_size; /* must be 256 (DefaultVMSettings) */
+    int32_t max_stack_frames; /* 8 */
+    uint64_t max_steps;       /* per-packet step budget; 0 = default (1<<20) */
+    uint32_t ingress_ifindex; /* xdp_md.ingress_ifindex seen by every packet (default 1) */
+    uint32_t rx_queue_index;  /* xdp_md.rx_queue_index (default 0) */
+    int32_t device;           /* HIP device ordinal */
+    uint32_t mode;            /* XE_MODE_* */
+} xe_settings;
+
+typedef struct xe_batch_stats {
+    uint64_t packets;
+    uint64_t steps;            /* instructions retired over the batch */
+    uint64_t status_count[8];  /* histogram of xe_result.status */
+    uint32_t mode_used;        /* XE_MODE_PARALLEL or XE_MODE_SEQUENTIAL */
+    uint32_t conflict;         /* 1 if the parallel run was order-dependent */
+    float kernel_ms;           /* device time of the interpreter launch(es) */
+    float total_ms;            /* device time of the whole call */
+} xe_batch_stats;
+
+typedef struct xe_vm xe_vm;
+
+/* --- VM lifetime --- */
+/* NewVM, emulator/vm.go:30-48 */
+int xe_default_settings(xe_settings* s);
+int xe_create(const xe_settings* s, xe_vm** out);
+void xe_destroy(xe_vm* vm);
+/* text of the last failed call on this vm */
+const char* xe_last_error(const xe_vm* vm);
+
+/* --- programs: AddRawProgram emulator/vm.go:61-73 (Decode + Translate) --- */
+/* insns: n raw 8-byte eBPF instructions (ebpf.RawInstruction, ebpf/ebpf.go:46-56).
+ * *prog_idx receives the 1-based program index (emulator/vm.go:36-38,56). */
+int xe_add_raw_program(xe_vm* vm, const uint64_t* insns, uint32_t n, int32_t* prog_idx);
+/* SetEntrypoint, emulator/vm.go:100-108 */
+int xe_set_entrypoint(xe_vm* vm, int32_t prog_idx);
+
+/* --- maps: AddMap / AddAbstractMap emulator/vm.go:75-98, AbstractMapToVM emulator/maps.go:85-156 --- */
+/* init/init_len: optional initial bytes of an ARRAY/PERCPU_ARRAY (ArrayMap.Init InitialData,
+ * emulator/maps_array.go:19-44). *map_idx receives the 1-based map index. */
+int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_len, int32_t* map_idx);
+/* host-side key/value access (Map.Lookup / Map.Update from Go userspace code):
+ * lookup returns 1 if found (value copied), 0 if absent. */
+int xe_map_lookup(xe_vm* vm, int32_t map_idx, const void* key, void* value_out);
+int xe_map_update(xe_vm* vm, int32_t map_idx, const void* key, const void* value);
+int xe_map_delete(xe_vm* vm, int32_t map_idx, const void* key);
+/* Final-state dump. ARRAY: raw ValueSize*MaxEntries bytes into `keys_or_raw`.
+ * HASH: entries sorted by key bytes; keys into keys_or_raw (count*key_size), values into values
+ * (count*value_size). Pass NULL buffers to query the count/byte size in *count / *bytes. */
+int xe_map_count(xe_vm* vm, int32_t map_idx, uint64_t* count);
+int xe_map_dump(xe_vm* vm, int32_t map_idx, void* keys_or_raw, void* values, uint64_t cap_entries,
+                uint64_t* count);
+
+/* --- running: the per-packet harness of SURVEY Appendix B over a batch ---
+ * Each packet i runs Reset; R1 = &MemoryPtr{ctx}; Run (emulator/vm.go:110-173, 211-246).
+ * Device-resident form: umem, desc, out (and regs if non-NULL) are device pointers.
+ * verdicts (device, optional) receives uint32(R0) per packet. */
+int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
+                        void* d_results, void* d_verdicts, void* d_regs, void* stream,
+                        xe_batch_stats* stats);
+/* Host-memory form (end-to-end: pinned staging + hipMemcpyAsync H2D/D2H). Packet writes made by the
+ * program are copied back into umem. results/regs may be NULL. */
+int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* desc, uint32_t n,
+                      xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);
+
+/* --- multi-GPU shard support: counter deltas for an RCCL all-reduce ---
+ * Values region of a map as a flat little-endian byte image (ARRAY: ValueSize*MaxEntries; HASH: the
+ * device slot table's values, identical layout on every replica built the same way). */
+int xe_map_values_bytes(xe_vm* vm, int32_t map_idx, uint64_t* bytes);
+/* d_out (device, bytes) := current values - snapshot taken at the start of the last run (u64 words) */
+int xe_map_delta(xe_vm* vm, int32_t map_idx, void* d_out, void* stream);
+/* values := snapshot + d_in (u64 words, wrapping) */
+int xe_map_apply_delta(xe_vm* vm, int32_t map_idx, const void* d_in, void* stream);
+/* footprint masks of the last run, for cross-shard conflict checks: 2 u64 per map (read, atomic) + flags */
+int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords);
+
+/* build / device info */
+const char* xe_version(void);
+int xe_device_count(int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XDPEMU_H */

@@ -67,6 +67,7 @@ def main() -> None:
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--cpu-sample", type=int, default=0, help="oracle baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--engine", default="auto", choices=["auto", "interp", "jit"])
     args = ap.parse_args()
 
     import torch
@@ -97,7 +98,8 @@ def main() -> None:
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
     del umem
 
-    vm = VM(Settings(device=local))
+    engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
+    vm = VM(Settings(device=local, engine=engine))
     W.setup_vm(vm, name)
     maps = list(vm.map_defs)
     deltas = {m: torch.zeros(vm.map_values_bytes(m) // 8, dtype=torch.int64, device=dev) for m in maps}
@@ -119,12 +121,13 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    kernel_ms, mode, conflicts, steps_retired, status_ok = [], set(), 0, 0, 0
+    kernel_ms, mode, conflicts, steps_retired, status_ok, engines = [], set(), 0, 0, 0, set()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(st["kernel_ms"])
         mode.add(st["mode_used"])
+        engines.add({1: "interp", 2: "jit"}.get(st["engine_used"], "?"))
         conflicts += st["conflict"]
         steps_retired += st["steps"]
         status_ok += st["status_count"][0]
@@ -167,10 +170,11 @@ def main() -> None:
             "config": {"workload": WORKLOADS[name],
                        "packets_per_gpu": n, "packet_size": hw, "parallelism": f"dp{world} (packet shards)",
                        "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
+                       "engine": sorted(engines),
                        "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel": "xe_jit_kernel" if engines == {"jit"} else "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "alg_bytes_per_packet": "16 desc + min(len,64) header + 4 verdict"},
             "cpu_baseline": cpu,

@@ -35,13 +35,14 @@ class MapDef(C.Structure):  # map_definition.go:15-27
 class Settings(C.Structure):  # emulator/vm.go:282-296 + device knobs
     _fields_ = [("stack_frame_size", C.c_int32), ("max_stack_frames", C.c_int32),
                 ("max_steps", C.c_uint64), ("ingress_ifindex", C.c_uint32),
-                ("rx_queue_index", C.c_uint32), ("device", C.c_int32), ("mode", C.c_uint32)]
+                ("rx_queue_index", C.c_uint32), ("device", C.c_int32), ("mode", C.c_uint32),
+                ("engine", C.c_uint32)]
 
 
 class BatchStats(C.Structure):
     _fields_ = [("packets", C.c_uint64), ("steps", C.c_uint64), ("status_count", C.c_uint64 * 8),
                 ("mode_used", C.c_uint32), ("conflict", C.c_uint32), ("kernel_ms", C.c_float),
-                ("total_ms", C.c_float)]
+                ("total_ms", C.c_float), ("engine_used", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 # numpy dtypes matching the structs (for zero-copy batch buffers)
@@ -120,5 +121,6 @@ def product() -> Lib:
     """The HIP product library. Raises if it is not built — there is no CPU fallback."""
     global _product
     if _product is None:
-        _product = Lib(PRODUCT_LIB, "xe_")
+        import os
+        _product = Lib(os.environ.get("XE_LIB", PRODUCT_LIB), "xe_")
     return _product

@@ -86,20 +86,45 @@ XE_DEV uint64_t xe_ctx_default_word(int w) {
        : 0x0606060605050505ull;
 }
 
-struct XeLane {
-  // registers R0..R10
-  int64_t rv[11];
-  uint32_t rh[11];
-  uint32_t rt[11];
-  // object table (ids 1..63; 1..6 are the ctx objects, materialised lazily)
+// per-lane memory in scratch: object table (ids 1..63; 1..6 are the xdp_md ctx objects,
+// materialised lazily) and the ValueMemory byte maps (object ids), reset lazily via XeLane::dirty
+struct XeMem {
   int64_t ov[XE_NOBJ];
   uint32_t oh[XE_NOBJ];
   uint32_t ot[XE_NOBJ];
-  uint64_t oused;     // allocated ids
-  uint64_t odef;      // ids 1..6 still holding their ctx default
-  // ValueMemory byte maps (ids), lazily reset
   uint64_t bm[XE_NWORDS];
-  uint64_t dirty;
+};
+
+struct XeReg {
+  int64_t v;   // RegisterValue.Value()
+  uint32_t h;  // memory handle (pointers)
+  uint32_t t;  // kind | readonly | alias id
+};
+
+#if defined(XE_REGS_FIELDS)
+// per-program kernels (JIT): every register index is a compile-time constant, so named fields fold
+// to plain VGPRs
+#define XE_REG_DECL XeReg r0, r1, r2, r3, r4, r5, r6, r7, r8, r9, r10;
+#elif defined(__HIPCC__)
+// interpreter kernel: vector values; element access with a wave-uniform index lowers to VGPR
+// indexing (s_set_gpr_idx) instead of a scratch-memory array
+typedef long long xe_v16l __attribute__((ext_vector_type(16)));
+typedef unsigned int xe_v16u __attribute__((ext_vector_type(16)));
+#define XE_REG_DECL xe_v16l rv; xe_v16u rh; xe_v16u rt;
+#else  // host simulation: plain arrays
+#define XE_REG_DECL long long rv[16]; unsigned int rh[16]; unsigned int rt[16];
+#endif
+
+struct XeLane {
+  // registers R0..R10 (see reg_get/reg_put)
+  XE_REG_DECL
+  // dynamically indexed lane memory (object table, byte maps): a separate struct so that the
+  // register fields above stay splittable into VGPRs (SROA gives up on aggregates with any
+  // variable-indexed member)
+  struct XeMem* mem;
+  uint64_t oused;     // allocated object ids
+  uint64_t odef;      // ids 1..6 still holding their ctx default
+  uint64_t dirty;     // ValueMemory words written since Reset
   // packet
   uint8_t* pkt;
   int64_t plen;
@@ -107,6 +132,36 @@ struct XeLane {
   uint64_t fpr[4];
   uint64_t fpa[4];
 };
+
+
+// ------------------------------------------------------------------ registers
+// By-value element access on the vector members: the index is wave-uniform (micro-op fields), so
+// the backend emits VGPR-indexed moves; with a constant index (helpers, JIT) it is a plain VGPR.
+#if defined(XE_REGS_FIELDS)
+XE_DEV XeReg reg_get(const XeLane& L, int i) {
+  switch (i) {
+    case 0: return L.r0; case 1: return L.r1; case 2: return L.r2; case 3: return L.r3;
+    case 4: return L.r4; case 5: return L.r5; case 6: return L.r6; case 7: return L.r7;
+    case 8: return L.r8; case 9: return L.r9; default: return L.r10;
+  }
+}
+XE_DEV void reg_put(XeLane& L, int i, const XeReg& r) {
+  switch (i) {
+    case 0: L.r0 = r; break; case 1: L.r1 = r; break; case 2: L.r2 = r; break; case 3: L.r3 = r; break;
+    case 4: L.r4 = r; break; case 5: L.r5 = r; break; case 6: L.r6 = r; break; case 7: L.r7 = r; break;
+    case 8: L.r8 = r; break; case 9: L.r9 = r; break; default: L.r10 = r; break;
+  }
+}
+#else
+XE_DEV XeReg reg_get(const XeLane& L, int i) {
+  return XeReg{int64_t(L.rv[i]), L.rh[i], L.rt[i]};
+}
+XE_DEV void reg_put(XeLane& L, int i, const XeReg& r) {
+  L.rv[i] = (long long)r.v;
+  L.rh[i] = r.h;
+  L.rt[i] = r.t;
+}
+#endif
 
 // ------------------------------------------------------------------ object table
 XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& t) {
@@ -117,15 +172,15 @@ XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& 
     v = id == 2 ? L.plen : 0;  // ingress/rxq filled by the caller through ov[] defaults below
     return;
   }
-  v = L.ov[id];
-  h = L.oh[id];
-  t = L.ot[id];
+  v = L.mem->ov[id];
+  h = L.mem->oh[id];
+  t = L.mem->ot[id];
 }
 
 XE_DEV void obj_set(XeLane& L, int id, int64_t v, uint32_t h, uint32_t t) {
-  L.ov[id] = v;
-  L.oh[id] = h;
-  L.ot[id] = t;
+  L.mem->ov[id] = v;
+  L.mem->oh[id] = h;
+  L.mem->ot[id] = t;
   L.odef &= ~(1ull << id);
 }
 
@@ -136,28 +191,31 @@ XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
     obj_get(L, id, ov, oh, ot);
     obj_set(L, id, v, oh, ot);
   } else {
-    L.ov[id] = v;
+    L.mem->ov[id] = v;
   }
 }
 
 XE_DEV uint64_t bm_word(const XeLane& L, int w) {
-  if ((L.dirty >> w) & 1ull) return L.bm[w];
+  if ((L.dirty >> w) & 1ull) return L.mem->bm[w];
   return w >= XE_CTX_WORD0 ? xe_ctx_default_word(w) : 0ull;
 }
 XE_DEV void bm_set_word(XeLane& L, int w, uint64_t v) {
-  L.bm[w] = v;
+  L.mem->bm[w] = v;
   L.dirty |= 1ull << w;
 }
 
 // mark-sweep collection of object ids when the table is full
 XE_DEV void obj_gc(XeLane& L) {
   uint64_t marks = 1ull;
+#pragma unroll 1
   for (int w = 0; w < XE_NWORDS; w++) {
     uint64_t word = bm_word(L, w);
+#pragma unroll 1
     for (int b = 0; b < 8; b++) marks |= 1ull << ((word >> (8 * b)) & 63u);
   }
+#pragma unroll
   for (int r = 0; r < 10; r++) {
-    uint32_t a = XE_T_ALIAS(L.rt[r]);
+    uint32_t a = XE_T_ALIAS(reg_get(L, r).t);
     if (a) marks |= 1ull << a;
   }
   marks |= 1ull;
@@ -172,24 +230,30 @@ XE_DEV int obj_alloc(XeLane& L) {
   return id;
 }
 
-// ------------------------------------------------------------------ registers
+// ------------------------------------------------------------------ register writes
 XE_DEV void reg_replace(XeLane& L, int d, uint32_t kind, uint32_t h, int64_t v, uint32_t alias_and_ro) {
-  L.rv[d] = v;
-  L.rh[d] = h;
-  L.rt[d] = kind | alias_and_ro;
+  reg_put(L, d, XeReg{v, h, kind | alias_and_ro});
+}
+
+// every register aliasing object `a` sees its new value
+XE_DEV void alias_refresh(XeLane& L, uint32_t a, int64_t v) {
+#pragma unroll
+  for (int j = 0; j < 10; j++) {
+    XeReg q = reg_get(L, j);
+    if (XE_T_ALIAS(q.t) == a) { q.v = v; reg_put(L, j, q); }
+  }
 }
 
 // RegisterValue.Assign on register d's object (in place; registers.go:194-197,243-247,305-313)
 XE_DEV int reg_inplace(XeLane& L, int d, int64_t v) {
-  uint32_t t = L.rt[d];
-  if (XE_T_KIND(t) == XE_KIND_FRAMEPTR && (t & XE_T_RO)) return XE_E_READONLY;
-  L.rv[d] = v;
-  uint32_t a = XE_T_ALIAS(t);
+  XeReg r = reg_get(L, d);
+  if (XE_T_KIND(r.t) == XE_KIND_FRAMEPTR && (r.t & XE_T_RO)) return XE_E_READONLY;
+  r.v = v;
+  reg_put(L, d, r);
+  uint32_t a = XE_T_ALIAS(r.t);
   if (a) {
     obj_set_val(L, int(a), v);
-#pragma unroll
-    for (int j = 0; j < 10; j++)
-      if (XE_T_ALIAS(L.rt[j]) == a) L.rv[j] = v;
+    alias_refresh(L, a, v);
   }
   return 0;
 }
@@ -261,6 +325,7 @@ XE_DEV uint64_t load_le(const uint8_t* p, int size) {
     }
   }
   uint64_t x = 0;
+#pragma unroll 1
   for (int b = 0; b < size; b++) x |= uint64_t(p[b]) << (8 * b);
   return x;
 }
@@ -275,6 +340,7 @@ XE_DEV void store_le(uint8_t* p, int size, uint64_t x) {
       default: *reinterpret_cast<uint64_t*>(p) = x; return;
     }
   }
+#pragma unroll 1
   for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
 }
 
@@ -290,6 +356,7 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
   uint64_t carry = 0;
   uintptr_t w = start & ~uintptr_t(3);
   int consumed = 0;  // field bytes consumed so far
+#pragma unroll 1
   while (w < end) {
     int lo = start > w ? int(start - w) : 0;
     int hi = end < w + 4 ? int(end - w) : 4;  // exclusive
@@ -331,6 +398,7 @@ XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id
   vmem_region(h, wb, len);
   if (int e = bounds(off, size, len)) return e;
   int first = vmem_byte(L, wb, off);
+#pragma unroll 1
   for (int i = 1; i < size; i++)
     if (vmem_byte(L, wb, off + i) != first) return XE_E_NONCONTIG;
   if (!first) return XE_E_UNINIT;
@@ -341,6 +409,7 @@ XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id
 XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
   int64_t end = off + size;
   int w0 = int(off >> 3), w1 = int((end - 1) >> 3);
+#pragma unroll 1
   for (int w = w0; w <= w1; w++) {
     int64_t lo = off > int64_t(w) * 8 ? off - int64_t(w) * 8 : 0;
     int64_t hi = end < int64_t(w + 1) * 8 ? end - int64_t(w) * 8 : 8;
@@ -402,19 +471,22 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
 // emit(i, byte) receives the output bytes. Returns 0 / XE_E_OOB / panic. dry = validate only.
 template <class Emit>
 XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Emit emit) {
-  uint32_t kind = XE_T_KIND(L.rt[r]);
-  uint32_t h = L.rh[r];
-  int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, L.rv[r]) : L.rv[r];
+  const XeReg R = reg_get(L, r);
+  uint32_t kind = XE_T_KIND(R.t);
+  uint32_t h = R.h;
+  int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R.v) : R.v;
   uint32_t c = xe_h_cls(h);
   if (c == XE_H_CTX || c == XE_H_STACK) {
     int wb; int64_t len;
     vmem_region(h, wb, len);
     if (off < 0 || xe_wadd(off, count) > len) return XE_E_OOB;
     if (off >= len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
+#pragma unroll 1
     for (int64_t i = 0; i < count;) {
       int v = vmem_byte(L, wb, off + i);
       if (!v) { emit(i, 0); i++; continue; }
       int size = 1;
+#pragma unroll 1
       for (int64_t j = i + 1; j < i + 8 && j < count; j++) {
         if (vmem_byte(L, wb, off + j) != v) break;
         size++;
@@ -423,6 +495,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
       if (i + w > count) return XE_EV_PANIC | XE_P_INDEX;
       int64_t ov; uint32_t oh, ot;
       obj_get(L, v, ov, oh, ot);
+#pragma unroll 1
       for (int b = 0; b < w; b++) emit(i + b, uint8_t(uint64_t(ov) >> (8 * b)));
       i += w;
     }
@@ -432,6 +505,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
   if (B.map && count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
+#pragma unroll 1
   for (int64_t i = 0; i < count; i++) emit(i, B.base[off + i]);
   return 0;
 }
@@ -442,11 +516,13 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
   uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(hv) & mask;
+#pragma unroll 1
   for (uint32_t probe = 0; probe < M.cap; probe++) {
     uint32_t st = M.state[idx];
     if (!(st & XE_SLOT_FULL)) return -1;
     const uint64_t* k = M.keys + uint64_t(idx) * M.kwords;
     bool eq = true;
+#pragma unroll 1
     for (uint32_t w = 0; w < M.kwords; w++) eq = eq && (k[w] == kw[w]);
     if (eq) return int64_t(idx);
     idx = (idx + 1) & mask;
@@ -489,10 +565,11 @@ XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint
 // ------------------------------------------------------------------ helpers
 // regToMap, helper_functions.go:109-130. m = 0 means "R0 := 0, helper returns nil".
 XE_DEV int reg_to_map(XeLane& L, const XeParams& P, uint32_t& m) {
-  int64_t idx = L.rv[1];
-  if (XE_T_KIND(L.rt[1]) == XE_KIND_MEMPTR) {
+  const XeReg R1 = reg_get(L, 1);
+  int64_t idx = R1.v;
+  if (XE_T_KIND(R1.t) == XE_KIND_MEMPTR) {
     uint32_t k, oh, al; int64_t v;
-    if (int e = mem_read(L, P, L.rh[1], L.rv[1], 4, true, k, oh, v, al)) return e;
+    if (int e = mem_read(L, P, R1.h, R1.v, 4, true, k, oh, v, al)) return e;
     idx = v;
   }
   if (idx < 1 || idx > int64_t(P.nmaps)) {
@@ -515,12 +592,13 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
   if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
   const XeDevMap& M = P.maps[m];
-  if (XE_T_KIND(L.rt[2]) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
+  const XeReg R2 = reg_get(L, 2);
+  if (XE_T_KIND(R2.t) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
   if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
-    uint32_t kind = XE_T_KIND(L.rt[2]);
-    int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, L.rv[2]) : L.rv[2];
+    uint32_t kind = XE_T_KIND(R2.t);
+    int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R2.v) : R2.v;
     uint32_t k, oh, al; int64_t kv;
-    int e = mem_read(L, P, L.rh[2], off, 4, true, k, oh, kv, al);
+    int e = mem_read(L, P, R2.h, off, 4, true, k, oh, kv, al);
     if (XE_IS_PANIC(e)) return e;
     if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;  // error ignored, nil keyValReg.Value()
     int64_t voff = xe_wmul(kv, int64_t(M.value_size));
@@ -547,15 +625,17 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
   if (!m) return 0;
   const XeDevMap& M = P.maps[m];
   if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
-    if (XE_T_KIND(L.rt[3]) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
-    if (XE_T_KIND(L.rt[2]) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
+    const XeReg R2 = reg_get(L, 2), R3 = reg_get(L, 3);
+    if (XE_T_KIND(R3.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
+    if (XE_T_KIND(R2.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     uint32_t k, oh, al; int64_t kv;
-    if (int e = mem_read(L, P, L.rh[2], L.rv[2], 4, true, k, oh, kv, al))
+    if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al))
       return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
     if (kv >= int64_t(M.vals_bytes)) return helper_errno_result(L, -7);
+#pragma unroll 1
     for (int64_t i = 0; i < int64_t(M.value_size); i++) {
       int64_t v;
-      if (int e = mem_read(L, P, L.rh[3], i, 1, true, k, oh, v, al))  // ignores the value ptr offset
+      if (int e = mem_read(L, P, R3.h, i, 1, true, k, oh, v, al))  // ignores the value ptr offset
         return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
       int64_t dst = xe_wadd(xe_wmul(kv, int64_t(M.value_size)), i);
       if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
@@ -565,13 +645,13 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
     return helper_errno_result(L, 0);
   }
   if (M.kind == XE_DM_HASH) {  // HashMap.Update, maps_hash.go:65-123
-    if (XE_T_KIND(L.rt[2]) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    if (XE_T_KIND(reg_get(L, 2).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
     if (int e = read_key(L, P, 2, M, kw, empty)) return e;
     int64_t slot = hash_find(M, kw, empty);
     if (slot < 0 && uint64_t(*M.count) + 1 > M.max_entries) return helper_errno_result(L, -7);
-    if (XE_T_KIND(L.rt[3]) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    if (XE_T_KIND(reg_get(L, 3).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
     // value ReadRange: validate first (a panic must leave the map untouched)
     int ve = ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t, uint8_t) {});
     if (XE_IS_PANIC(ve)) return ve;
@@ -682,9 +762,152 @@ XE_DEV bool jmp_cond(uint32_t op, bool wide, int64_t d, int64_t s) {
 }
 
 // effective offset of a pointer register + insn offset (inst_load.go:91-101)
-XE_DEV int64_t ptr_eff(const XeLane& L, int r, int32_t ioff) {
-  return XE_T_KIND(L.rt[r]) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(256, L.rv[r]), ioff)
-                                                 : xe_wadd(L.rv[r], ioff);
+XE_DEV int64_t ptr_eff(const XeReg& R, int32_t ioff) {
+  return XE_T_KIND(R.t) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(256, R.v), ioff) : xe_wadd(R.v, ioff);
+}
+
+// ---- per-class handlers (exec_uop dispatches; the JIT calls them directly with constant uops)
+XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u) {
+  const int d = u.dst, s = u.src;
+  const bool wide = u.fl & UF_WIDE, reg = u.fl & UF_REG;
+  const XeReg D = reg_get(L, d);
+  const XeReg S = reg ? reg_get(L, s) : XeReg{int64_t(u.imm), 0, 0};
+  if (reg && u.x == 0x00 && XE_T_KIND(S.t) != XE_KIND_IMM) {
+    // inst_add.go:82-98,131-147: dst becomes a Copy of the pointer src with the sum as offset
+    int64_t v = wide ? xe_wadd(D.v, S.v) : int64_t(int32_t(uint32_t(xe_i32(D.v)) + uint32_t(xe_i32(S.v))));
+    reg_replace(L, d, XE_T_KIND(S.t), S.h, v, 0);
+    return 0;
+  }
+  if ((u.x == 0x30 || u.x == 0x90) && S.v == 0) return XE_E_DIV0;
+  int64_t v;
+  if (int e = alu_compute(u.x, wide, D.v, S.v, v)) return e;
+  return reg_inplace(L, d, v);
+}
+
+XE_DEV int uop_movi(XeLane& L, const XeUop& u) {
+  reg_replace(L, u.dst, XE_KIND_IMM, 0, int64_t(u.imm), 0);
+  return 0;
+}
+
+XE_DEV int uop_movr(XeLane& L, const XeUop& u) {
+  const XeReg S = reg_get(L, u.src);
+  reg_replace(L, u.dst, XE_T_KIND(S.t), S.h, S.v, 0);
+  return 0;
+}
+
+XE_DEV int uop_neg(XeLane& L, const XeUop& u) {
+  const int64_t dv = reg_get(L, u.dst).v;
+  int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(xe_i32(dv))));
+  return reg_inplace(L, u.dst, v);
+}
+
+XE_DEV int uop_end(XeLane& L, const XeUop& u) {
+  uint64_t rv = uint64_t(reg_get(L, u.dst).v), v;
+  if (u.x == 0) {
+    v = u.imm == 16 ? uint64_t(__builtin_bswap16(uint16_t(rv)))
+      : u.imm == 32 ? uint64_t(__builtin_bswap32(uint32_t(rv))) : __builtin_bswap64(rv);
+  } else {
+    v = u.imm == 16 ? uint64_t(uint16_t(rv)) : u.imm == 32 ? uint64_t(uint32_t(rv)) : rv;
+  }
+  return reg_inplace(L, u.dst, int64_t(v));
+}
+
+// returns whether the branch is taken
+XE_DEV bool uop_jmp(const XeLane& L, const XeUop& u) {
+  const bool wide = u.fl & UF_WIDE;
+  const XeReg D = reg_get(L, u.dst);
+  if (u.fl & UF_REG) {
+    const XeReg S = reg_get(L, u.src);
+    bool same = XE_T_KIND(D.t) == XE_T_KIND(S.t);
+    bool c = jmp_cond(u.x, wide, D.v, S.v);
+    return u.x == 0x50 ? (!same || c) : (same && c);
+  }
+  bool imm = XE_T_KIND(D.t) == XE_KIND_IMM;
+  bool c = jmp_cond(u.x, wide, D.v, int64_t(u.imm));
+  return u.x == 0x50 ? (!imm || c) : (imm && c);
+}
+
+XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u) {
+  const int d = u.dst, s = u.src;
+  if (s == 1) { reg_replace(L, d, XE_KIND_IMM, 0, int64_t(uint32_t(u.imm)), 0); return 0; }
+  if (s == 2) {  // BPF_PSEUDO_MAP_FD_VALUE, inst_load.go:36-63
+    uint32_t m = uint32_t(u.imm);
+    if (uint64_t(m) >= uint64_t(P.nmaps) + 1) return XE_E_NO_MAP;
+    if (m == 0) return XE_EV_PANIC | XE_P_NIL_MAP;
+    const XeDevMap& M = P.maps[m];
+    if (M.kind == XE_DM_ARRAY) {
+      if (M.vals_bytes == 0) return XE_E_MAP_NOT_PTR;
+      reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), int64_t(u.x), 0);
+      return 0;
+    }
+    if (M.kind == XE_DM_HASH) {
+      uint64_t kw[XE_MAX_KEY / 8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      bool empty = M.key_size > 4 || M.key_size == 0;  // ReadRange of a 4-byte tmp memory
+      int64_t slot = hash_find(M, kw, empty);
+      if (slot < 0) return XE_E_MAP_NOT_PTR;
+      reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), int64_t(u.x), 0);
+      return 0;
+    }
+    return XE_EV_UNSUP;
+  }
+  return reg_inplace(L, d, int64_t((uint64_t(u.x) << 32) + uint64_t(uint32_t(u.imm))));
+}
+
+XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u) {
+  const XeReg S = reg_get(L, u.src);
+  if (XE_T_KIND(S.t) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
+  uint32_t kind, oh, al; int64_t v;
+  if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), true, kind, oh, v, al)) return e;
+  if (u.fl & UF_BADDST) return XE_E_ASSIGN_REG;
+  reg_replace(L, u.dst, kind, oh, v, al);
+  return 0;
+}
+
+// ST (u.cls == U_ST, value = imm) and STX
+XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u) {
+  const XeReg D = reg_get(L, u.dst);
+  if (XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  const bool st = u.cls == U_ST;
+  const XeReg S = st ? XeReg{int64_t(u.imm), 0, uint32_t(XE_KIND_IMM)} : reg_get(L, u.src);
+  return mem_write(L, P, D.h, ptr_eff(D, u.tgt), uop_size(u), XE_T_KIND(S.t), S.h, S.v);
+}
+
+XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
+  const XeReg D = reg_get(L, u.dst);
+  if (XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  const uint32_t h = D.h;
+  const int64_t off = ptr_eff(D, u.tgt);
+  const int size = uop_size(u);
+  const uint32_t c = xe_h_cls(h);
+  if (c == XE_H_CTX || c == XE_H_STACK) {
+    int id = 0;
+    if (int e = vmem_read(L, h, off, size, id)) return e;
+    if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+    int64_t ov; uint32_t oh, ot;
+    obj_get(L, id, ov, oh, ot);
+    if (XE_T_KIND(ot) == XE_KIND_FRAMEPTR && (ot & XE_T_RO)) return XE_E_READONLY;
+    int64_t nv = xe_wadd(ov, reg_get(L, u.src).v);
+    obj_set_val(L, id, nv);
+    alias_refresh(L, uint32_t(id), nv);
+    return 0;
+  }
+  XeBMem B;
+  bmem_resolve(L, P, h, B);
+  if (int e = bounds(off, size, B.len)) return e;
+  if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+  const uint64_t add = uint64_t(reg_get(L, u.src).v);
+  if (B.map) {
+    fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
+    atomic_add_field(B.base + off, size, add);
+  } else {
+    uint64_t cur = load_le(B.base + off, size);
+    store_le(B.base + off, size, cur + add);
+  }
+  return 0;
+}
+
+XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u) {
+  return call_helper(L, P, u.cls == U_HELPER ? int64_t(u.imm) : reg_get(L, u.dst).v);
 }
 
 // ------------------------------------------------------------------ one instruction
@@ -692,136 +915,24 @@ XE_DEV int64_t ptr_eff(const XeLane& L, int r, int32_t ioff) {
 // before Step's increment), XE_EV_EXIT, or an error code.
 XE_DEV int exec_uop(XeLane& L, const XeParams& P, const XeUop& u, int32_t pc, int32_t& tgt) {
   tgt = pc;
-  const int d = u.dst, s = u.src;
   switch (u.cls) {
     case U_FAIL: return u.imm;
     case U_NOP: return 0;
     case U_EXIT: return XE_EV_EXIT;
     case U_JA: tgt = u.tgt; return 0;
-    case U_ALU: {
-      bool wide = u.fl & UF_WIDE, reg = u.fl & UF_REG;
-      int64_t dv = L.rv[d];
-      int64_t sv = reg ? L.rv[s] : int64_t(u.imm);
-      if (reg && u.x == 0x00 && XE_T_KIND(L.rt[s]) != XE_KIND_IMM) {
-        // inst_add.go:82-98,131-147: dst becomes a Copy of the pointer src with the sum as offset
-        int64_t v = wide ? xe_wadd(dv, sv) : int64_t(int32_t(uint32_t(xe_i32(dv)) + uint32_t(xe_i32(sv))));
-        reg_replace(L, d, XE_T_KIND(L.rt[s]), L.rh[s], v, 0);
-        return 0;
-      }
-      if ((u.x == 0x30 || u.x == 0x90) && sv == 0) return XE_E_DIV0;
-      int64_t v;
-      if (int e = alu_compute(u.x, wide, dv, sv, v)) return e;
-      return reg_inplace(L, d, v);
-    }
-    case U_MOVI: reg_replace(L, d, XE_KIND_IMM, 0, int64_t(u.imm), 0); return 0;
-    case U_MOVR: reg_replace(L, d, XE_T_KIND(L.rt[s]), L.rh[s], L.rv[s], 0); return 0;
-    case U_NEG: {
-      int64_t dv = L.rv[d];
-      int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(xe_i32(dv))));
-      return reg_inplace(L, d, v);
-    }
-    case U_END: {
-      uint64_t rv = uint64_t(L.rv[d]), v;
-      if (u.x == 0) {
-        v = u.imm == 16 ? uint64_t(__builtin_bswap16(uint16_t(rv)))
-          : u.imm == 32 ? uint64_t(__builtin_bswap32(uint32_t(rv))) : __builtin_bswap64(rv);
-      } else {
-        v = u.imm == 16 ? uint64_t(uint16_t(rv)) : u.imm == 32 ? uint64_t(uint32_t(rv)) : rv;
-      }
-      return reg_inplace(L, d, int64_t(v));
-    }
-    case U_JMP: {
-      bool wide = u.fl & UF_WIDE;
-      int64_t dv = L.rv[d];
-      bool taken;
-      if (u.fl & UF_REG) {
-        bool same = XE_T_KIND(L.rt[d]) == XE_T_KIND(L.rt[s]);
-        bool c = jmp_cond(u.x, wide, dv, L.rv[s]);
-        taken = u.x == 0x50 ? (!same || c) : (same && c);
-      } else {
-        bool imm = XE_T_KIND(L.rt[d]) == XE_KIND_IMM;
-        bool c = jmp_cond(u.x, wide, dv, int64_t(u.imm));
-        taken = u.x == 0x50 ? (!imm || c) : (imm && c);
-      }
-      if (taken) tgt = u.tgt;
-      return 0;
-    }
-    case U_LDIMM64: {
-      if (s == 1) { reg_replace(L, d, XE_KIND_IMM, 0, int64_t(uint32_t(u.imm)), 0); return 0; }
-      if (s == 2) {  // BPF_PSEUDO_MAP_FD_VALUE, inst_load.go:36-63
-        uint32_t m = uint32_t(u.imm);
-        if (uint64_t(m) >= uint64_t(P.nmaps) + 1) return XE_E_NO_MAP;
-        if (m == 0) return XE_EV_PANIC | XE_P_NIL_MAP;
-        const XeDevMap& M = P.maps[m];
-        if (M.kind == XE_DM_ARRAY) {
-          if (M.vals_bytes == 0) return XE_E_MAP_NOT_PTR;
-          reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), int64_t(u.x), 0);
-          return 0;
-        }
-        if (M.kind == XE_DM_HASH) {
-          uint64_t kw[XE_MAX_KEY / 8] = {0, 0, 0, 0, 0, 0, 0, 0};
-          bool empty = M.key_size > 4 || M.key_size == 0;  // ReadRange of a 4-byte tmp memory
-          int64_t slot = hash_find(M, kw, empty);
-          if (slot < 0) return XE_E_MAP_NOT_PTR;
-          reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), int64_t(u.x), 0);
-          return 0;
-        }
-        return XE_EV_UNSUP;
-      }
-      return reg_inplace(L, d, int64_t((uint64_t(u.x) << 32) + uint64_t(uint32_t(u.imm))));
-    }
-    case U_LDX: {
-      if (XE_T_KIND(L.rt[s]) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
-      int64_t off = ptr_eff(L, s, u.tgt);
-      uint32_t kind, oh, al; int64_t v;
-      if (int e = mem_read(L, P, L.rh[s], off, uop_size(u), true, kind, oh, v, al)) return e;
-      if (u.fl & UF_BADDST) return XE_E_ASSIGN_REG;
-      reg_replace(L, d, kind, oh, v, al);
-      return 0;
-    }
-    case U_ST: {
-      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
-      return mem_write(L, P, L.rh[d], ptr_eff(L, d, u.tgt), uop_size(u), XE_KIND_IMM, 0, int64_t(u.imm));
-    }
-    case U_STX: {
-      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
-      return mem_write(L, P, L.rh[d], ptr_eff(L, d, u.tgt), uop_size(u), XE_T_KIND(L.rt[s]), L.rh[s], L.rv[s]);
-    }
-    case U_ATOMIC: {
-      if (XE_T_KIND(L.rt[d]) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
-      uint32_t h = L.rh[d];
-      int64_t off = ptr_eff(L, d, u.tgt);
-      int size = uop_size(u);
-      uint32_t c = xe_h_cls(h);
-      if (c == XE_H_CTX || c == XE_H_STACK) {
-        int id = 0;
-        if (int e = vmem_read(L, h, off, size, id)) return e;
-        if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
-        int64_t ov; uint32_t oh, ot;
-        obj_get(L, id, ov, oh, ot);
-        if (XE_T_KIND(ot) == XE_KIND_FRAMEPTR && (ot & XE_T_RO)) return XE_E_READONLY;
-        int64_t nv = xe_wadd(ov, L.rv[s]);
-        obj_set_val(L, id, nv);
-#pragma unroll
-        for (int j = 0; j < 10; j++)
-          if (XE_T_ALIAS(L.rt[j]) == uint32_t(id)) L.rv[j] = nv;
-        return 0;
-      }
-      XeBMem B;
-      bmem_resolve(L, P, h, B);
-      if (int e = bounds(off, size, B.len)) return e;
-      if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
-      if (B.map) {
-        fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
-        atomic_add_field(B.base + off, size, uint64_t(L.rv[s]));
-      } else {
-        uint64_t cur = load_le(B.base + off, size);
-        store_le(B.base + off, size, cur + uint64_t(L.rv[s]));
-      }
-      return 0;
-    }
-    case U_HELPER: return call_helper(L, P, int64_t(u.imm));
-    case U_CALLX: return call_helper(L, P, L.rv[d]);
+    case U_ALU: return uop_alu(L, P, u);
+    case U_MOVI: return uop_movi(L, u);
+    case U_MOVR: return uop_movr(L, u);
+    case U_NEG: return uop_neg(L, u);
+    case U_END: return uop_end(L, u);
+    case U_JMP: if (uop_jmp(L, u)) tgt = u.tgt; return 0;
+    case U_LDIMM64: return uop_ldimm64(L, P, u);
+    case U_LDX: return uop_ldx(L, P, u);
+    case U_ST:
+    case U_STX: return uop_store(L, P, u);
+    case U_ATOMIC: return uop_atomic(L, P, u);
+    case U_HELPER:
+    case U_CALLX: return uop_helper(L, P, u);
     case U_CALLBPF: return XE_EV_UNSUP;
   }
   return XE_EV_UNSUP;
@@ -840,10 +951,9 @@ XE_DEV int wave_min(int v) {
   return cur;
 }
 
-// Runs the per-packet harness for packet index `i` on this lane (valid=false:
-// the lane idles). All lanes of the wave must call this together.
-XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
-  // ---- Reset (emulator/vm.go:211-246) + harness ctx
+// Reset (emulator/vm.go:211-246) + the per-packet harness ctx for packet `i`.
+XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+#pragma unroll
   for (int r = 0; r < 10; r++) reg_replace(L, r, XE_KIND_IMM, 0, 0, 0);
   reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
   reg_replace(L, 1, XE_KIND_MEMPTR, xe_h_make(XE_H_CTX, 0, 0), 0, 0);
@@ -862,7 +972,71 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   // ingress / rx queue objects are IMMs with settings values: materialise them eagerly
   obj_set(L, 4, int64_t(P.ingress), 0, XE_KIND_IMM);
   obj_set(L, 5, int64_t(P.rxq), 0, XE_KIND_IMM);
+}
 
+// map an exec_uop error to the lane's final status/code
+XE_DEV void status_from_error(int e, int& status, int& code) {
+  if (e == XE_EV_EXIT) { status = XE_ST_OK; }
+  else if (XE_EV_CLASS(e) == XE_EV_ORD) { status = XE_ST_INTERNAL_ORDERED; }
+  else if (XE_EV_CLASS(e) == XE_EV_CAP) { status = XE_ST_CAPACITY; }
+  else if (XE_EV_CLASS(e) == XE_EV_UNSUP) { status = XE_ST_UNSUPPORTED; }
+  else if (XE_IS_PANIC(e)) { status = XE_ST_PANIC; code = e & 0xff; }
+  else { status = XE_ST_VMERR; code = e & 0xffff; }
+}
+
+// results, parity record, flags and batch statistics for the lane's packet (all lanes call this)
+XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, int status, int code,
+                        int32_t res_pc, uint64_t steps) {
+  if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
+  if (status == XE_ST_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
+  if (valid) {
+    const XeReg R0 = reg_get(L, 0);
+    if (P.results) {
+      xe_result r;
+      r.status = uint8_t(status);
+      r.r0_kind = uint8_t(XE_T_KIND(R0.t));
+      r.code = uint16_t(code);
+      r.pc = uint32_t(res_pc);
+      r.r0 = R0.v;
+      P.results[i] = r;
+    }
+    if (P.verdicts) P.verdicts[i] = uint32_t(uint64_t(R0.v));
+    if (P.regs) {
+      xe_regs g;
+#pragma unroll
+      for (int r = 0; r < 10; r++) {
+        const XeReg R = reg_get(L, r);
+        g.val[r] = R.v;
+        uint32_t k = XE_T_KIND(R.t);
+        g.kind[r] = uint8_t(k);
+        if (k == XE_KIND_IMM) { g.region[r] = 0xff; g.map[r] = 0; }
+        else {
+          uint32_t c = xe_h_cls(R.h);
+          g.region[r] = uint8_t(c);
+          g.map[r] = uint8_t((c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(R.h) : 0);
+        }
+      }
+      g.pad[0] = g.pad[1] = 0;
+      g.steps = uint32_t(steps);
+      P.regs[i] = g;
+    }
+  }
+  // batch statistics: one atomic per wave per counter
+  unsigned long long my_steps = valid ? steps : 0;
+#if defined(__HIPCC__)
+  for (int o = 32; o > 0; o >>= 1) my_steps += __shfl_xor(my_steps, o);
+#endif
+  if (xe_lane() == 0 && my_steps) xe_atomic_add64(&P.stats[0], my_steps);
+  for (int st = 0; st < 8; st++) {
+    unsigned long long c = __builtin_popcountll(xe_ballot(valid && status == st));
+    if (c && xe_lane() == 0) xe_atomic_add64(&P.stats[1 + st], c);
+  }
+}
+
+// Interpreter engine: runs the harness for packet `i` on this lane (valid=false: the lane idles).
+// All lanes of the wave must call this together.
+XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+  lane_reset(L, P, i, valid);
   int status = valid ? -1 : XE_ST_OK;  // -1 = running
   int code = 0;
   int32_t pc = 0, res_pc = 0;
@@ -889,70 +1063,19 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
           } else {
             pc = tgt + 1;
           }
-        } else if (e == XE_EV_EXIT) {
-          status = XE_ST_OK;
-        } else if (XE_EV_CLASS(e) == XE_EV_ORD) {
-          status = XE_ST_INTERNAL_ORDERED;
-        } else if (XE_EV_CLASS(e) == XE_EV_CAP) {
-          status = XE_ST_CAPACITY;
-        } else if (XE_EV_CLASS(e) == XE_EV_UNSUP) {
-          status = XE_ST_UNSUPPORTED;
-        } else if (XE_IS_PANIC(e)) {
-          status = XE_ST_PANIC; code = e & 0xff;
         } else {
-          status = XE_ST_VMERR; code = e & 0xffff;
+          status_from_error(e, status, code);
         }
       }
     }
   }
-
-  if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
-  if (status == XE_ST_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
-  if (valid) {
-    if (P.results) {
-      xe_result r;
-      r.status = uint8_t(status);
-      r.r0_kind = uint8_t(XE_T_KIND(L.rt[0]));
-      r.code = uint16_t(code);
-      r.pc = uint32_t(res_pc);
-      r.r0 = L.rv[0];
-      P.results[i] = r;
-    }
-    if (P.verdicts) P.verdicts[i] = uint32_t(uint64_t(L.rv[0]));
-    if (P.regs) {
-      xe_regs g;
-      for (int r = 0; r < 10; r++) {
-        g.val[r] = L.rv[r];
-        uint32_t k = XE_T_KIND(L.rt[r]);
-        g.kind[r] = uint8_t(k);
-        if (k == XE_KIND_IMM) { g.region[r] = 0xff; g.map[r] = 0; }
-        else {
-          uint32_t c = xe_h_cls(L.rh[r]);
-          g.region[r] = uint8_t(c);
-          g.map[r] = uint8_t((c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(L.rh[r]) : 0);
-        }
-      }
-      g.pad[0] = g.pad[1] = 0;
-      g.steps = uint32_t(steps);
-      P.regs[i] = g;
-    }
-  }
-  // batch statistics: one atomic per wave per counter
-  unsigned long long my_steps = valid ? steps : 0;
-#if defined(__HIPCC__)
-  for (int o = 32; o > 0; o >>= 1) my_steps += __shfl_xor(my_steps, o);
-#endif
-  if (xe_lane() == 0 && my_steps) xe_atomic_add64(&P.stats[0], my_steps);
-  for (int st = 0; st < 8; st++) {
-    unsigned long long c = __builtin_popcountll(xe_ballot(valid && status == st));
-    if (c && xe_lane() == 0) xe_atomic_add64(&P.stats[1 + st], c);
-  }
+  lane_finish(L, P, i, valid, status, code, res_pc, steps);
 }
 
 // flush per-lane footprints of maps 1..4 to global (wave OR-reduction, one atomic per word)
 XE_DEV void flush_footprints(XeLane& L, const XeParams& P) {
+#pragma unroll
   for (int k = 0; k < 4; k++) {
-    if (uint32_t(k + 1) > P.nmaps) break;
     unsigned long long r = L.fpr[k], a = L.fpa[k];
 #if defined(__HIPCC__)
     for (int o = 32; o > 0; o >>= 1) { r |= __shfl_xor(r, o); a |= __shfl_xor(a, o); }

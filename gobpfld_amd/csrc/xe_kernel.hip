@@ -7,7 +7,9 @@
 #include "xe_interp.h"
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
+  XeMem M;
   XeLane L;
+  L.mem = &M;
 #pragma unroll
   for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
   const int lane = xe_lane();

@@ -27,6 +27,8 @@ typedef hipStream_t xe_stream_t;
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
+extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, bool* cyclic, const char** err);
+extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 #endif
 
 namespace {
@@ -41,7 +43,9 @@ int d2d(void* d, const void* s, size_t n, xe_stream_t) { memmove(d, s, n); retur
 int dmemset(void* d, int v, size_t n, xe_stream_t) { memset(d, v, n); return 0; }
 int dsync(xe_stream_t) { return 0; }
 int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
+  XeMem M;
   XeLane L;
+  L.mem = &M;
   for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
@@ -50,6 +54,7 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   flush_footprints(L, *P);
   return 0;
 }
+int launch_jit(void*, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return launch_interp(P, b, t, s); }
 int launch_delta(const void* cur, const void* snap, void* out, uint64_t nw, xe_stream_t) {
   for (uint64_t i = 0; i < nw; i++) ((uint64_t*)out)[i] = ((const uint64_t*)cur)[i] - ((const uint64_t*)snap)[i];
   return 0;
@@ -75,6 +80,7 @@ int d2d(void* d, const void* src, size_t n, xe_stream_t s) { return hipMemcpyAsy
 int dmemset(void* d, int v, size_t n, xe_stream_t s) { return hipMemsetAsync(d, v, n, s) == hipSuccess ? 0 : -1; }
 int dsync(xe_stream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -1; }
 int launch_interp(const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_launch_interp(P, b, t, s); }
+int launch_jit(void* fn, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_jit_launch(fn, P, b, t, s); }
 int launch_delta(const void* c, const void* sn, void* o, uint64_t nw, xe_stream_t s) { return xe_launch_delta(c, sn, o, nw, s); }
 int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t nw, xe_stream_t s) { return xe_launch_apply_delta(c, sn, d, nw, s); }
 struct Timer {
@@ -321,6 +327,11 @@ struct xe_vm {
   void* d_regs = nullptr; size_t d_regs_cap = 0;
   std::vector<unsigned long long> last_fp;
   uint32_t last_flags = 0;
+  // per-program kernel (JIT engine) for the current entry program
+  int32_t jit_idx = -1;
+  void* jit_fn = nullptr;
+  bool jit_cyclic = false;
+  std::string jit_error;
   Timer t0, t1, t2;
 };
 
@@ -688,6 +699,27 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   P.fp = vm->d_aux + 32;
 
   const uint32_t mode = vm->settings.mode;
+  uint32_t engine = vm->settings.engine;
+  if (const char* env = getenv("XE_ENGINE")) engine = !strcmp(env, "interp") ? XE_ENGINE_INTERP : !strcmp(env, "jit") ? XE_ENGINE_JIT : engine;
+  void* jit = nullptr;
+#ifndef XE_HOSTSIM
+  if (engine != XE_ENGINE_INTERP) {
+    if (vm->jit_idx != vm->entry) {
+      const auto& prog = vm->programs[vm->entry];
+      const char* jerr = "";
+      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, &vm->jit_cyclic, &jerr);
+      vm->jit_error = jerr ? jerr : "";
+      vm->jit_idx = vm->entry;
+    }
+    jit = vm->jit_fn;
+    // acyclic kernels carry no budget checks: exact only while the budget cannot be reached
+    if (jit && !vm->jit_cyclic && vm->settings.max_steps < vm->d_prog_len) jit = nullptr;
+    if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
+  }
+#endif
+  auto launch = [&](const XeParams* p, uint32_t b, uint32_t t) {
+    return jit ? launch_jit(jit, p, b, t, s) : launch_interp(p, b, t, s);
+  };
   // snapshot map values: rollback point for the ordered fallback and base of the shard deltas
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
@@ -700,10 +732,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   if (mode == XE_MODE_SEQUENTIAL) {
     P.mode = XE_MODE_SEQUENTIAL;
     used = XE_MODE_SEQUENTIAL;
-    if (launch_interp(&P, 1, 64, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   } else {
     P.mode = XE_MODE_PARALLEL;
-    if (launch_interp(&P, grid_blocks(n), 256, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    if (launch(&P, grid_blocks(n), 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   }
   vm->t1.rec(s);
   std::vector<unsigned long long> aux(kAuxWords);
@@ -724,7 +756,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       P.mode = XE_MODE_SEQUENTIAL;
       used = XE_MODE_SEQUENTIAL;
       vm->t1.rec(s);
-      if (launch_interp(&P, 1, 64, s)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+      if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t2.rec(s);
       if (d2h(aux.data(), vm->d_aux, kAuxWords * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
       kms += Timer::ms(vm->t1, vm->t2);
@@ -741,6 +773,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     stats->conflict = conflict ? 1 : 0;
     stats->kernel_ms = kms;
     stats->total_ms = kms;
+    stats->engine_used = jit ? XE_ENGINE_JIT : XE_ENGINE_INTERP;
   }
   return XE_OK;
 }
@@ -810,6 +843,16 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
   out[0] = vm->last_flags;
   for (uint32_t i = 0; i < 2 * nm; i++) out[1 + i] = i < vm->last_fp.size() ? vm->last_fp[i] : 0;
   return XE_OK;
+}
+
+// debug/inspection: translate raw eBPF into micro-ops (returns count, or a negative XE_ERR_*)
+int xe_translate_uops(const uint64_t* insns, uint32_t n, void* out, uint32_t cap) {
+  std::vector<XeUop> prog;
+  std::string err;
+  int rc = translate(insns, n, prog, err);
+  if (rc) return rc;
+  if (out && cap >= prog.size()) memcpy(out, prog.data(), prog.size() * sizeof(XeUop));
+  return int(prog.size());
 }
 
 const char* xe_version(void) {

@@ -23,6 +23,7 @@ from . import _native as N
 STATUS = {0: "OK", 1: "VMERR", 2: "PANIC", 3: "BUDGET", 4: "UNSUPPORTED", 5: "CAPACITY"}
 MAP_HASH, MAP_ARRAY, MAP_PROG_ARRAY, MAP_PERF_EVENT_ARRAY, MAP_PERCPU_HASH, MAP_PERCPU_ARRAY = 1, 2, 3, 4, 5, 6
 MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL = 0, 1, 2
+ENGINE_AUTO, ENGINE_INTERP, ENGINE_JIT = 0, 1, 2
 
 
 class EmulatorError(RuntimeError):
@@ -47,6 +48,7 @@ class Settings:
     rx_queue_index: int = 0
     device: int = 0
     mode: int = MODE_AUTO
+    engine: int = 0  # ENGINE_AUTO
 
 
 @dataclass
@@ -60,7 +62,7 @@ class BatchResult:
 def _stats_dict(s: N.BatchStats) -> dict:
     return {"packets": s.packets, "steps": s.steps, "status_count": list(s.status_count),
             "mode_used": s.mode_used, "conflict": s.conflict, "kernel_ms": s.kernel_ms,
-            "total_ms": s.total_ms}
+            "total_ms": s.total_ms, "engine_used": s.engine_used}
 
 
 class VM:
@@ -71,7 +73,7 @@ class VM:
         self.lib.default_settings(C.byref(cs)) if self.lib.has("default_settings") else None
         cs.stack_frame_size, cs.max_stack_frames = 256, 8
         cs.max_steps, cs.ingress_ifindex, cs.rx_queue_index = s.max_steps, s.ingress_ifindex, s.rx_queue_index
-        cs.device, cs.mode = s.device, s.mode
+        cs.device, cs.mode, cs.engine = s.device, s.mode, s.engine
         self.settings = s
         h = C.c_void_p()
         rc = self.lib.create(C.byref(cs), C.byref(h))

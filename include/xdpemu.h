@@ -96,6 +96,11 @@ extern "C" {
 #define XE_MAP_QUEUE 22
 #define XE_MAP_STACK 23
 
+/* engines */
+#define XE_ENGINE_AUTO 0   /* per-program gfx950 kernel (hiprtc), interpreter if it cannot be built */
+#define XE_ENGINE_INTERP 1 /* shared micro-op interpreter kernel */
+#define XE_ENGINE_JIT 2    /* per-program kernel only (error if it cannot be built) */
+
 /* run modes */
 #define XE_MODE_AUTO 0       /* parallel, verified; falls back to ordered device execution on conflict */
 #define XE_MODE_PARALLEL 1   /* parallel only; conflicts reported in stats, results kept            */
@@ -145,6 +150,7 @@ typedef struct xe_settings {
     uint32_t rx_queue_index;  /* xdp_md.rx_queue_index (default 0) */
     int32_t device;           /* HIP device ordinal */
     uint32_t mode;            /* XE_MODE_* */
+    uint32_t engine;          /* XE_ENGINE_* */
 } xe_settings;
 
 typedef struct xe_batch_stats {
@@ -155,6 +161,8 @@ typedef struct xe_batch_stats {
     uint32_t conflict;         /* 1 if the parallel run was order-dependent */
     float kernel_ms;           /* device time of the interpreter launch(es) */
     float total_ms;            /* device time of the whole call */
+    uint32_t engine_used;      /* XE_ENGINE_INTERP or XE_ENGINE_JIT */
+    uint32_t reserved;
 } xe_batch_stats;
 
 typedef struct xe_vm xe_vm;

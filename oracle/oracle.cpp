@@ -210,6 +210,92 @@ static bool translate(const std::vector<Inst>& prog, std::string& err) {
   return true;
 }
 
+
+// Go String() of each decoded instruction (ebpf/*.go String methods), used to pin the decoder
+// against the reference fixture ebpf/asm_test.bpfasm (TestDecodeEncodeSymmetry, ebpf/asm_test.go).
+static const char* kHelperNames[] = {
+    "", "bpf_map_lookup_elem", "bpf_map_update_elem", "bpf_map_delete_elem", "bpf_probe_read",
+    "bpf_ktime_get_ns", "bpf_trace_printk", "bpf_get_prandom_u32", "bpf_get_smp_processor_id",
+    "bpf_skb_store_bytes", "bpf_l3_csum_replace", "bpf_l4_csum_replace", "bpf_tail_call",
+    "bpf_clone_redirect", "bpf_get_current_pid_tgid", "bpf_get_current_uid_gid",
+    "bpf_get_current_comm", "bpf_get_cgroup_classid", "bpf_skb_vlan_push", "bpf_skb_vlan_pop",
+    "bpf_skb_get_tunnel_key", "bpf_skb_set_tunnel_key", "bpf_perf_event_read", "bpf_redirect",
+    "bpf_get_route_realm", "bpf_perf_event_output", "bpf_skb_load_bytes", "bpf_get_stackid",
+    "bpf_csum_diff", "bpf_skb_get_tunnel_opt", "bpf_skb_set_tunnel_opt", "bpf_skb_change_proto",
+    "bpf_skb_change_type", "bpf_skb_under_cgroup", "bpf_get_hash_recalc", "bpf_get_current_task",
+    "bpf_probe_write_user"};
+
+static std::string regName(int r) { return r < 11 ? std::to_string(r) : std::string("invalid"); }
+static const char* sizeName(uint8_t s) {
+  switch (s) { case 0x00: return "u32"; case 0x08: return "u16"; case 0x10: return "u8"; case 0x18: return "u64"; }
+  return "invalid";
+}
+static std::string signedOff(int64_t off) {  // "+ 456" / "- 456"
+  return off < 0 ? "- " + std::to_string(-off) : "+ " + std::to_string(off);
+}
+static std::string plusd(int64_t v) { return (v >= 0 ? "+" : "") + std::to_string(v); }  // Go %+d
+
+static std::string goString(const Inst& i) {
+  std::string d = regName(i.dst), s = regName(i.src);
+  const char* p = i.wide ? "r" : "w";
+  switch (i.k) {
+    case K_LDIMM64:
+      if (i.src == 1) return "r" + d + " = map fd#" + std::to_string(i.val1);
+      if (i.src == 2) return "r" + d + " = map value#" + std::to_string(i.val1) + "[" + std::to_string(i.val2) + "]";
+      return "r" + d + " = " + std::to_string((uint64_t(i.val2) << 32) + uint64_t(i.val1)) + " ll";
+    case K_NOP: return "nop";
+    case K_LDABS: return std::string("r0 = ntohl((") + sizeName(i.size) + ") (((struct sk_buff *) r6)->data[" + std::to_string(i.imm) + "]))";
+    case K_LDIND: return std::string("r0 = ntohl((") + sizeName(i.size) + ") (((struct sk_buff *) r6)->data[r" + s + " " + signedOff(i.imm) + "]))";
+    case K_LDX: return "r" + d + " = *(" + sizeName(i.size) + " *)(r" + s + " " + signedOff(i.off) + ")";
+    case K_ST: return std::string("*(") + sizeName(i.size) + " *)(r" + d + " " + signedOff(i.off) + ") = " + std::to_string(i.imm);
+    case K_STX: return std::string("*(") + sizeName(i.size) + " *)(r" + d + " " + signedOff(i.off) + ") = r" + s;
+    case K_ATOMIC: {
+      std::string reg = i.size == 0x00 ? "w" : "r";
+      std::string mem = std::string("*(") + sizeName(i.size) + " *)(r" + d + " " + signedOff(i.off) + ")";
+      switch (i.op & 0xfe) {
+        case 0x00: return "lock " + mem + " += " + reg + s;
+        case 0x10: return "lock " + mem + " -= " + reg + s;
+        case 0x50: return "lock " + mem + " &= " + reg + s;
+        case 0x40: return "lock " + mem + " |= " + reg + s;
+        case 0xa0: return "lock " + mem + " ^= " + reg + s;
+        case 0xe0: return reg + s + " = xchg(r" + d + " " + signedOff(i.off) + ", " + reg + s + ")";
+        case 0xf0: return reg + "0 = cmpxchg(r" + d + " " + signedOff(i.off) + ", " + reg + "0, " + reg + s + ")";
+      }
+      return "?";
+    }
+    case K_ALU: {
+      const char* op = "?";
+      switch (i.op) {
+        case OP_ADD: op = "+="; break; case OP_SUB: op = "-="; break; case OP_MUL: op = "*="; break;
+        case OP_DIV: op = "/="; break; case OP_OR: op = "|="; break; case OP_AND: op = "&="; break;
+        case OP_LSH: op = "<<="; break; case OP_RSH: op = ">>="; break; case OP_MOD: op = "%="; break;
+        case OP_XOR: op = "^="; break; case OP_MOV: op = "="; break; case OP_ARSH: op = "s>>="; break;
+      }
+      std::string rhs = i.reg ? std::string(p) + s : std::to_string(i.imm);
+      return std::string(p) + d + " " + op + " " + rhs;
+    }
+    case K_NEG: return std::string(p) + d + " = -" + p + d;
+    case K_END: return "r" + d + " = " + (i.op ? "be" : "le") + std::to_string(i.imm) + " r" + d;
+    case K_JA: return "goto " + plusd(i.off);
+    case K_JMP: {
+      const char* op = "?";
+      switch (i.op) {
+        case J_JEQ: op = "=="; break; case J_JGT: op = ">"; break; case J_JGE: op = ">="; break;
+        case J_JSET: op = "&"; break; case J_JNE: op = "!="; break; case J_JSGT: op = "s>"; break;
+        case J_JSGE: op = "s>="; break; case J_JLT: op = "<"; break; case J_JLE: op = "<="; break;
+        case J_JSLT: op = "s<"; break; case J_JSLE: op = "s<="; break;
+      }
+      std::string rhs = i.reg ? std::string(p) + s : std::to_string(i.imm);
+      return std::string("if ") + p + d + " " + op + " " + rhs + " goto " + plusd(i.off);
+    }
+    case K_CALL: return "call " + std::to_string(i.imm) + "#" + ((i.imm >= 0 && i.imm <= 36) ? kHelperNames[i.imm] : "");
+    case K_CALLBPF: return "call " + plusd(i.imm);
+    case K_CALLX: return "callx r" + regName(uint8_t(i.imm));
+    case K_EXIT: return "exit";
+  }
+  return "?";
+}
+
 // ---------------------------------------------------------------- values & memory
 struct Memory;
 struct RV {  // RegisterValue, emulator/registers.go:151-166
@@ -1080,6 +1166,19 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
   // drop references to this batch's packet/ctx memories
   reset(&vm);
   if (stats) stats->mode_used = XE_MODE_SEQUENTIAL;
+  return XE_OK;
+}
+
+int orc_decode_text(const uint64_t* insns, uint32_t n, char* buf, size_t buflen) {
+  std::vector<Inst> prog;
+  std::string err, out;
+  if (!decode(insns, n, prog, err)) return XE_ERR_DECODE;
+  for (auto& i : prog) out += goString(i) + "\n";
+  if (buf && buflen) {
+    size_t c = std::min(buflen - 1, out.size());
+    memcpy(buf, out.data(), c);
+    buf[c] = 0;
+  }
   return XE_OK;
 }
 

@@ -30,6 +30,8 @@ int orc_run_batch(orc_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* d
                   xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);
 /* decode-only entry for decoder KATs: writes one type-name line per decoded instruction into buf
  * (ebpf.Instruction %T names, e.g. "Add64Register"); returns XE_OK / XE_ERR_DECODE / XE_ERR_TRANSLATE */
+/* decode + Go String() rendering of every instruction (one per line) */
+int orc_decode_text(const uint64_t* insns, uint32_t n, char* buf, size_t buflen);
 int orc_decode_names(const uint64_t* insns, uint32_t n, char* buf, size_t buflen);
 #ifdef __cplusplus
 }

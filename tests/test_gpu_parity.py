@@ -8,43 +8,51 @@ import numpy as np
 import pytest
 
 from gobpfld_amd import workloads as W
-from gobpfld_amd.emulator import MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
+from gobpfld_amd.emulator import ENGINE_INTERP, ENGINE_JIT, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
 from kats import KATS
 from parity import assert_same, config_case, packets, run_one
 
 pytestmark = pytest.mark.gpu
+ENGINES = [ENGINE_INTERP, ENGINE_JIT]
+ENGINE_IDS = ["interp", "jit"]
 
 
+@pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("k", KATS, ids=[k["name"] for k in KATS])
-def test_kat_device_equals_oracle(gpu_lib, oracle_lib, k):
+def test_kat_device_equals_oracle(gpu_lib, oracle_lib, k, engine):
     umem, descs = packets(64, k["pkt"], seed=7)
-    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"])
+    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"], settings=Settings(engine=engine))
+    assert a[0].stats["engine_used"] == engine
     b = run_one(oracle_lib, k["program"], k["maps"], umem, descs, entries=k["entries"])
     assert_same(a, b, k["name"])
 
 
+@pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("name,n,cap", [("c1", 1024, None), ("c2", 65536, None), ("c3", 30000, 8192),
                                         ("c4", 8192, None), ("c5", 30000, 8192)])
-def test_config_device_equals_oracle(gpu_lib, oracle_lib, name, n, cap):
+def test_config_device_equals_oracle(gpu_lib, oracle_lib, name, n, cap, engine):
     prog, maps, entries, umem, descs = config_case(name, n, cap)
-    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries)
+    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=Settings(engine=engine))
+    assert a[0].stats["engine_used"] == engine
     b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries)
     assert_same(a, b, name)
     assert a[0].stats["mode_used"] == MODE_PARALLEL, "commutative config must run in parallel mode"
 
 
-def test_sequential_mode_equals_oracle(gpu_lib, oracle_lib):
+@pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
+def test_sequential_mode_equals_oracle(gpu_lib, oracle_lib, engine):
     prog, maps, entries, umem, descs = config_case("c2", 2048)
-    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=Settings(mode=MODE_SEQUENTIAL))
+    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=Settings(mode=MODE_SEQUENTIAL, engine=engine))
     b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries)
     assert_same(a, b, "c2 sequential")
     assert a[0].stats["mode_used"] == MODE_SEQUENTIAL
 
 
-def test_ordered_program_falls_back(gpu_lib, oracle_lib):
+@pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
+def test_ordered_program_falls_back(gpu_lib, oracle_lib, engine):
     k = next(k for k in KATS if k["name"] == "nonatomic_rmw_on_map_value_ordered")
     umem, descs = packets(3000, 64, seed=3)
-    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs)
+    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, settings=Settings(engine=engine))
     b = run_one(oracle_lib, k["program"], k["maps"], umem, descs)
     assert_same(a, b, "ordered rmw")
     assert a[0].stats["conflict"] == 1 and a[0].stats["mode_used"] == MODE_SEQUENTIAL

@@ -4,10 +4,14 @@
 // map descriptors and the hash-table layout. Portable between hipcc (device + host) and g++ (the
 // test-only host simulation build, XE_HOSTSIM).
 #pragma once
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
+#endif
 #include "../../include/xdpemu.h"
 
-#if defined(__HIPCC__)
+#if defined(__HIPCC_RTC__)
+#define XE_HD __host__ __device__ __forceinline__
+#elif defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define XE_HD __host__ __device__ __forceinline__
 #else

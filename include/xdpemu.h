@@ -18,8 +18,21 @@
 #ifndef XDPEMU_H
 #define XDPEMU_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stddef.h>
 #include <stdint.h>
+#else /* hiprtc (per-program kernels): no C library headers */
+typedef unsigned char uint8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef unsigned long long uint64_t;
+typedef signed char int8_t;
+typedef short int16_t;
+typedef int int32_t;
+typedef long long int64_t;
+typedef unsigned long uintptr_t;
+typedef __SIZE_TYPE__ size_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -26,6 +26,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0
 WORKLOADS = {
+    "c1": "C1: 3-insn XDP_PASS (r0 = 2; r0 += 0; exit), 64 B packets, no maps",
     "c2": "C2 (BASELINE configs[1]): ~40-insn L2/L3 parse->PASS/DROP classifier, per-proto ARRAY counters",
     "c3": "C3: 5-tuple HASH lookup -> REDIRECT + hit counter, 64K flows, IMIX 64/576/1500 B",
     "c4": "C4: ~200-insn JEQ/JGT ACL (48 rules), 1500 B packets, lane-divergence stress",

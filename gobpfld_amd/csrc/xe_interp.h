@@ -131,6 +131,11 @@ struct XeLane {
   // per-lane map footprints for maps 1..4 (others go straight to global)
   uint64_t fpr[4];
   uint64_t fpa[4];
+  // xdp_md ingress_ifindex / rx_queue_index values of the lazily materialised ctx objects 4, 5
+  uint32_t ingress, rxq;
+  // wave-uniform batch statistics, flushed once per wave (flush_wave_state)
+  uint64_t acc_steps;
+  uint32_t acc_status[8];
 };
 
 
@@ -169,7 +174,7 @@ XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& 
     // xdp_md objects: data, data_end, data_meta = MemoryPtr{pkt}, then 3 IMMs
     h = id <= 3 ? xe_h_make(XE_H_PKT, 0, 0) : 0u;
     t = id <= 3 ? uint32_t(XE_KIND_MEMPTR) : uint32_t(XE_KIND_IMM);
-    v = id == 2 ? L.plen : 0;  // ingress/rxq filled by the caller through ov[] defaults below
+    v = id == 2 ? L.plen : id == 4 ? int64_t(L.ingress) : id == 5 ? int64_t(L.rxq) : 0;
     return;
   }
   v = L.mem->ov[id];
@@ -378,6 +383,37 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
     consumed += nb;
     w += 4;
   }
+}
+
+// Map atomics from the lanes active at this instruction, aggregated per distinct (address, size):
+// one leader lane adds the sum of its peers' addends (exact: the field add is modulo 2^(8*size), so
+// the sum of several adds equals one add of their sum). Removes same-address contention for hot
+// counters (C2's per-proto array, hot flows).
+XE_DEV void wave_atomic_add_field(uint8_t* p, int size, uint64_t add) {
+#if defined(__HIPCC__)
+  const uint64_t addr = uint64_t(uintptr_t(p));
+  unsigned long long remaining = xe_ballot(true);
+  const int me = xe_lane();
+  while (remaining) {
+    const int leader = __builtin_ctzll(remaining);
+    const uint64_t la = (uint64_t(uint32_t(xe_readlane(int(addr >> 32), leader))) << 32) |
+                        uint64_t(uint32_t(xe_readlane(int(uint32_t(addr)), leader)));
+    const int ls = xe_readlane(size, leader);
+    const unsigned long long peers = xe_ballot(addr == la && size == ls) & remaining;
+    uint64_t sum = 0;
+    unsigned long long m = peers;
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      sum += (uint64_t(uint32_t(xe_readlane(int(add >> 32), l))) << 32) |
+             uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), l)));
+    }
+    if (me == leader) atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(la)), ls, sum);
+    remaining &= ~peers;
+  }
+#else
+  atomic_add_field(p, size, add);
+#endif
 }
 
 // ------------------------------------------------------------------ ValueMemory access
@@ -898,7 +934,7 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   const uint64_t add = uint64_t(reg_get(L, u.src).v);
   if (B.map) {
     fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
-    atomic_add_field(B.base + off, size, add);
+    wave_atomic_add_field(B.base + off, size, add);
   } else {
     uint64_t cur = load_le(B.base + off, size);
     store_le(B.base + off, size, cur + add);
@@ -969,9 +1005,8 @@ XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
     L.pkt = P.umem + a;
     L.plen = int64_t(l);
   }
-  // ingress / rx queue objects are IMMs with settings values: materialise them eagerly
-  obj_set(L, 4, int64_t(P.ingress), 0, XE_KIND_IMM);
-  obj_set(L, 5, int64_t(P.rxq), 0, XE_KIND_IMM);
+  L.ingress = P.ingress;
+  L.rxq = P.rxq;
 }
 
 // map an exec_uop error to the lane's final status/code
@@ -1021,16 +1056,18 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
       P.regs[i] = g;
     }
   }
-  // batch statistics: one atomic per wave per counter
-  unsigned long long my_steps = valid ? steps : 0;
-#if defined(__HIPCC__)
-  for (int o = 32; o > 0; o >>= 1) my_steps += __shfl_xor(my_steps, o);
-#endif
-  if (xe_lane() == 0 && my_steps) xe_atomic_add64(&P.stats[0], my_steps);
-  for (int st = 0; st < 8; st++) {
-    unsigned long long c = __builtin_popcountll(xe_ballot(valid && status == st));
-    if (c && xe_lane() == 0) xe_atomic_add64(&P.stats[1 + st], c);
-  }
+  // batch statistics: per-lane step sums and wave-uniform status counts, flushed once per wave
+  L.acc_steps += valid ? steps : 0;
+#pragma unroll
+  for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
+}
+
+XE_DEV void wave_state_init(XeLane& L) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  L.acc_steps = 0;
+#pragma unroll
+  for (int st = 0; st < 8; st++) L.acc_status[st] = 0;
 }
 
 // Interpreter engine: runs the harness for packet `i` on this lane (valid=false: the lane idles).
@@ -1072,8 +1109,19 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   lane_finish(L, P, i, valid, status, code, res_pc, steps);
 }
 
-// flush per-lane footprints of maps 1..4 to global (wave OR-reduction, one atomic per word)
-XE_DEV void flush_footprints(XeLane& L, const XeParams& P) {
+// flush per-lane footprints of maps 1..4 (wave OR-reduction) and the batch statistics: one atomic
+// per word per wave
+XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
+  unsigned long long steps = L.acc_steps;
+#if defined(__HIPCC__)
+  for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o);
+#endif
+  if (xe_lane() == 0) {
+    if (steps) xe_atomic_add64(&P.stats[0], steps);
+#pragma unroll
+    for (int st = 0; st < 8; st++)
+      if (L.acc_status[st]) xe_atomic_add64(&P.stats[1 + st], L.acc_status[st]);
+  }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     unsigned long long r = L.fpr[k], a = L.fpa[k];

@@ -10,8 +10,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   XeMem M;
   XeLane L;
   L.mem = &M;
-#pragma unroll
-  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  wave_state_init(L);
   const int lane = xe_lane();
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
@@ -27,7 +26,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
       run_packet(L, P, i, i < P.n);
     }
   }
-  flush_footprints(L, P);
+  flush_wave_state(L, P);
 }
 
 extern "C" __global__ void xe_delta_kernel(const unsigned long long* cur, const unsigned long long* snap,

@@ -46,12 +46,12 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeMem M;
   XeLane L;
   L.mem = &M;
-  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  wave_state_init(L);
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
     run_packet(L, *P, i, true);
   }
-  flush_footprints(L, *P);
+  flush_wave_state(L, *P);
   return 0;
 }
 int launch_jit(void*, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return launch_interp(P, b, t, s); }

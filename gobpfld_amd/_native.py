@@ -68,6 +68,7 @@ _SIGS = {
     "map_lookup": (C.c_int, [P, C.c_int32, P, P]),
     "map_update": (C.c_int, [P, C.c_int32, P, P]),
     "map_delete": (C.c_int, [P, C.c_int32, P]),
+    "map_update_batch": (C.c_int, [P, C.c_int32, P, P, C.c_uint64]),
     "map_count": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_dump": (C.c_int, [P, C.c_int32, P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "run_batch": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),  # oracle form
@@ -86,7 +87,7 @@ _SIGS = {
 HEADER_SYMBOLS = [
     "xe_default_settings", "xe_create", "xe_destroy", "xe_last_error", "xe_add_raw_program",
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
-    "xe_map_count", "xe_map_dump", "xe_run_batch_device", "xe_run_batch_host",
+    "xe_map_count", "xe_map_dump", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
     "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_footprint", "xe_version",
     "xe_device_count",
 ]

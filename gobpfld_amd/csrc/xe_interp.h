@@ -55,6 +55,19 @@ XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return __
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 #endif
 
+// map kinds present in the VM (the per-program kernel sets these from the VM's maps, so helper paths
+// for absent kinds are compiled out; the interpreter keeps both)
+#ifndef XE_HAS_ARRAY
+#define XE_HAS_ARRAY 1
+#endif
+#ifndef XE_HAS_HASH
+#define XE_HAS_HASH 1
+#endif
+
+// packet header window staged in LDS per lane (the first 64 bytes are the hot bytes)
+#define XE_HDR_WIN 64
+#define XE_HDR_STRIDE 68  // 17 dwords: lanes reading the same offset hit distinct banks
+
 // kernel-internal error encoding
 #define XE_EV_PANIC 0x1000
 #define XE_EV_UNSUP 0x2000
@@ -128,6 +141,8 @@ struct XeLane {
   // packet
   uint8_t* pkt;
   int64_t plen;
+  uint8_t* hdr;      // LDS copy of the first min(plen, 64) packet bytes
+  int32_t hdr_len;
   // per-lane map footprints for maps 1..4 (others go straight to global)
   uint64_t fpr[4];
   uint64_t fpa[4];
@@ -267,7 +282,8 @@ XE_DEV int reg_inplace(XeLane& L, int d, int64_t v) {
 XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
   uint64_t vs = M.value_size;
   if (vs == 0) return ~0ull;
-  uint64_t o = array ? uint64_t(off) % vs : uint64_t(off);
+  uint64_t o = !array ? uint64_t(off)
+             : (uint64_t(off) >> 32) == 0 ? uint64_t(uint32_t(off) % uint32_t(vs)) : uint64_t(off) % vs;
   uint64_t e = o + uint64_t(size);  // exclusive
   if (e > vs) return ~0ull;         // straddles two values
   uint64_t lo, hi;
@@ -299,12 +315,14 @@ struct XeBMem {
 };
 
 XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem& B) {
+  // map memories only (packet accesses take the header-window path)
   uint32_t c = xe_h_cls(h);
-  if (c == XE_H_PKT) { B.base = L.pkt; B.len = L.plen; B.map = 0; B.array = false; return true; }
   uint32_t m = xe_h_map(h);
   const XeDevMap& M = P.maps[m];
   B.map = m;
-  if (c == XE_H_ARRAY) { B.base = M.vals; B.len = int64_t(M.vals_bytes); B.array = true; return true; }
+  if (!XE_HAS_HASH || (XE_HAS_ARRAY && c == XE_H_ARRAY)) {
+    B.base = M.vals; B.len = int64_t(M.vals_bytes); B.array = true; return true;
+  }
   uint32_t slot = xe_h_slot(h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
   B.len = (M.state[slot] & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
@@ -347,6 +365,35 @@ XE_DEV void store_le(uint8_t* p, int size, uint64_t x) {
   }
 #pragma unroll 1
   for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
+}
+
+// reads/writes of the LDS header copy (4-byte aligned base per lane)
+XE_DEV uint64_t hdr_read(const uint8_t* p, int size) {
+  const uintptr_t a = uintptr_t(p);
+  if (size == 1) return *p;
+  if (size == 2 && (a & 1) == 0) return *reinterpret_cast<const uint16_t*>(p);
+  if ((a & 3) == 0) {
+    if (size == 4) return *reinterpret_cast<const uint32_t*>(p);
+    if (size == 8) return uint64_t(reinterpret_cast<const uint32_t*>(p)[0]) | (uint64_t(reinterpret_cast<const uint32_t*>(p)[1]) << 32);
+  }
+  uint64_t x = 0;
+#pragma unroll 1
+  for (int b = 0; b < size; b++) x |= uint64_t(p[b]) << (8 * b);
+  return x;
+}
+XE_DEV void hdr_write(uint8_t* p, int size, uint64_t x) {
+#pragma unroll 1
+  for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
+}
+
+// packet ByteMemory access through the header window when possible
+XE_DEV uint64_t pkt_load(const XeLane& L, int64_t off, int size) {
+  if (off + size <= L.hdr_len) return hdr_read(L.hdr + off, size);
+  return load_le(L.pkt + off, size);
+}
+XE_DEV void pkt_store(XeLane& L, int64_t off, int size, uint64_t x) {
+  store_le(L.pkt + off, size, x);
+  if (off + size <= L.hdr_len) hdr_write(L.hdr + off, size, x);
 }
 
 // Atomic little-endian add of `add` into the `size`-byte field at p (any alignment), truncating
@@ -470,10 +517,18 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
     alias = (uint32_t(id) << 8) | (t & XE_T_RO);
     return 0;
   }
+  if (c == XE_H_PKT) {
+    if (int e = bounds(off, size, L.plen)) return e;
+    val = int64_t(pkt_load(L, off, size));
+    kind = XE_KIND_IMM;
+    oh = 0;
+    alias = 0;
+    return 0;
+  }
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (B.map && track) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, size));
+  if (track) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, size));
   val = int64_t(load_le(B.base + off, size));
   kind = XE_KIND_IMM;
   oh = 0;
@@ -495,10 +550,15 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
     vmem_fill(L, wb, off, size, id);
     return 0;
   }
+  if (c == XE_H_PKT) {
+    if (int e = bounds(off, size, L.plen)) return e;
+    pkt_store(L, off, size, uint64_t(val));
+    return 0;
+  }
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (B.map && P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // non-commutative shared write
+  if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // non-commutative shared write
   store_le(B.base + off, size, uint64_t(val));
   return 0;
 }
@@ -537,10 +597,16 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
     }
     return 0;
   }
+  if (c == XE_H_PKT) {
+    if (off < 0 || xe_wadd(off, count) > L.plen) return XE_E_OOB;
+#pragma unroll 1
+    for (int64_t i = 0; i < count; i++) emit(i, uint8_t(pkt_load(L, off + i, 1)));
+    return 0;
+  }
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
-  if (B.map && count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
+  if (count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
 #pragma unroll 1
   for (int64_t i = 0; i < count; i++) emit(i, B.base[off + i]);
   return 0;
@@ -630,7 +696,7 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
   const XeDevMap& M = P.maps[m];
   const XeReg R2 = reg_get(L, 2);
   if (XE_T_KIND(R2.t) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
-  if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
+  if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
     uint32_t kind = XE_T_KIND(R2.t);
     int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R2.v) : R2.v;
     uint32_t k, oh, al; int64_t kv;
@@ -642,7 +708,7 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
     else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), voff, 0);
     return 0;
   }
-  if (M.kind == XE_DM_HASH) {  // HashMap.Lookup, maps_hash.go:44-63
+  if (XE_HAS_HASH && M.kind == XE_DM_HASH) {  // HashMap.Lookup, maps_hash.go:44-63
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
     if (int e = read_key(L, P, 2, M, kw, empty)) return e;
@@ -660,7 +726,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
   if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
   const XeDevMap& M = P.maps[m];
-  if (M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
+  if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
     const XeReg R2 = reg_get(L, 2), R3 = reg_get(L, 3);
     if (XE_T_KIND(R3.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     if (XE_T_KIND(R2.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
@@ -680,7 +746,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
     }
     return helper_errno_result(L, 0);
   }
-  if (M.kind == XE_DM_HASH) {  // HashMap.Update, maps_hash.go:65-123
+  if (XE_HAS_HASH && M.kind == XE_DM_HASH) {  // HashMap.Update, maps_hash.go:65-123
     if (XE_T_KIND(reg_get(L, 2).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
@@ -871,12 +937,12 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u) {
     if (uint64_t(m) >= uint64_t(P.nmaps) + 1) return XE_E_NO_MAP;
     if (m == 0) return XE_EV_PANIC | XE_P_NIL_MAP;
     const XeDevMap& M = P.maps[m];
-    if (M.kind == XE_DM_ARRAY) {
+    if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {
       if (M.vals_bytes == 0) return XE_E_MAP_NOT_PTR;
       reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), int64_t(u.x), 0);
       return 0;
     }
-    if (M.kind == XE_DM_HASH) {
+    if (XE_HAS_HASH && M.kind == XE_DM_HASH) {
       uint64_t kw[XE_MAX_KEY / 8] = {0, 0, 0, 0, 0, 0, 0, 0};
       bool empty = M.key_size > 4 || M.key_size == 0;  // ReadRange of a 4-byte tmp memory
       int64_t slot = hash_find(M, kw, empty);
@@ -927,18 +993,18 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
     alias_refresh(L, uint32_t(id), nv);
     return 0;
   }
+  if (c == XE_H_PKT) {
+    if (int e = bounds(off, size, L.plen)) return e;
+    if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+    pkt_store(L, off, size, pkt_load(L, off, size) + uint64_t(reg_get(L, u.src).v));
+    return 0;
+  }
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
-  const uint64_t add = uint64_t(reg_get(L, u.src).v);
-  if (B.map) {
-    fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
-    wave_atomic_add_field(B.base + off, size, add);
-  } else {
-    uint64_t cur = load_le(B.base + off, size);
-    store_le(B.base + off, size, cur + add);
-  }
+  fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
+  wave_atomic_add_field(B.base + off, size, uint64_t(reg_get(L, u.src).v));
   return 0;
 }
 
@@ -998,12 +1064,27 @@ XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   L.odef = 0x7eull;
   L.pkt = P.umem;
   L.plen = 0;
+  L.hdr_len = 0;
   if (valid) {
     xe_desc dsc = P.desc[i];
     uint64_t a = dsc.addr, l = dsc.len;
     if (a > P.umem_len || l > P.umem_len - a) l = 0;
     L.pkt = P.umem + a;
     L.plen = int64_t(l);
+    // stage the header window: 16 independent dword loads when aligned and inside the buffer
+    const int hl = l < XE_HDR_WIN ? int(l) : XE_HDR_WIN;
+    L.hdr_len = hl;
+    if ((a & 3) == 0 && a + XE_HDR_WIN <= P.umem_len) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(L.pkt);
+      uint32_t w[XE_HDR_WIN / 4];
+#pragma unroll
+      for (int k = 0; k < XE_HDR_WIN / 4; k++) w[k] = src[k];
+#pragma unroll
+      for (int k = 0; k < XE_HDR_WIN / 4; k++) reinterpret_cast<uint32_t*>(L.hdr)[k] = w[k];
+    } else {
+#pragma unroll 1
+      for (int b = 0; b < hl; b++) L.hdr[b] = L.pkt[b];
+    }
   }
   L.ingress = P.ingress;
   L.rxq = P.rxq;

@@ -7,9 +7,11 @@
 #include "xe_interp.h"
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[256 * XE_HDR_STRIDE];
   XeMem M;
   XeLane L;
   L.mem = &M;
+  L.hdr = hdr_lds + threadIdx.x * XE_HDR_STRIDE;
   wave_state_init(L);
   const int lane = xe_lane();
   if (P.mode == XE_MODE_SEQUENTIAL) {

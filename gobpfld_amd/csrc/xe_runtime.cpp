@@ -27,7 +27,7 @@ typedef hipStream_t xe_stream_t;
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
-extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, bool* cyclic, const char** err);
+extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, unsigned mapkinds, bool* cyclic, const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 #endif
 
@@ -46,6 +46,8 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeMem M;
   XeLane L;
   L.mem = &M;
+  uint8_t hdrbuf[XE_HDR_STRIDE];
+  L.hdr = hdrbuf;
   wave_state_init(L);
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
@@ -557,6 +559,7 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
   }
   m.host_dirty = true;
   vm->maps.push_back(std::move(m));
+  vm->jit_idx = -1;  // map kinds are compiled into the per-program kernel
   if (idx) *idx = int32_t(vm->maps.size() - 1);
   return XE_OK;
 }
@@ -604,6 +607,15 @@ int xe_map_update(xe_vm* vm, int32_t mi, const void* key, const void* value) {
     memcpy(m->vals.data() + uint64_t(s) * m->def.value_size, value, m->def.value_size);
   }
   m->host_dirty = true;
+  return XE_OK;
+}
+
+int xe_map_update_batch(xe_vm* vm, int32_t mi, const void* keys, const void* values, uint64_t count) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || (count && (!keys || !values))) return XE_ERR_INVAL;
+  const size_t ks = m->dkind == XE_DM_ARRAY ? 4 : m->def.key_size, vs = m->def.value_size;
+  for (uint64_t i = 0; i < count; i++)
+    if (int rc = xe_map_update(vm, mi, (const uint8_t*)keys + i * ks, (const uint8_t*)values + i * vs)) return rc;
   return XE_OK;
 }
 
@@ -707,7 +719,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (vm->jit_idx != vm->entry) {
       const auto& prog = vm->programs[vm->entry];
       const char* jerr = "";
-      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, &vm->jit_cyclic, &jerr);
+      unsigned kinds = 0;
+      for (size_t i = 1; i < vm->maps.size(); i++) kinds |= vm->maps[i].dkind == XE_DM_ARRAY ? 1u : vm->maps[i].dkind == XE_DM_HASH ? 2u : 0u;
+      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, kinds, &vm->jit_cyclic, &jerr);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
     }

@@ -128,6 +128,15 @@ class VM:
         v = bytes(value).ljust(d.value_size, b"\0")
         self._check(self.lib.map_update(self.h, m, k, v), "map update")
 
+    def map_update_batch(self, m: int, keys: np.ndarray, values: np.ndarray) -> None:
+        """Bulk update: keys (n, key_size) and values (n, value_size) uint8 arrays."""
+        d = self.map_defs[m]
+        ks = d.key_size if d.type in (MAP_HASH, MAP_PERCPU_HASH, 13) else 4
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, ks)
+        v = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1, d.value_size)
+        assert len(k) == len(v)
+        self._check(self.lib.map_update_batch(self.h, m, k.ctypes.data, v.ctypes.data, len(k)), "map update batch")
+
     def map_lookup(self, m: int, key: bytes) -> bytes | None:
         d = self.map_defs[m]
         k = bytes(key).ljust(max(d.key_size, 4), b"\0")

@@ -441,9 +441,12 @@ def build_batch(name: str, start: int, n: int, hdr: int = 64):
         if np.all(sizes == sizes[0]) and sizes[0] >= hdr:
             umem[:total].reshape(n, int(sizes[0]))[:, :hdr] = h
         else:
-            for i in range(n):
-                L = min(hdr, int(sizes[i]))
-                umem[offs[i]:offs[i] + L] = h[i, :L]
+            cols = np.arange(hdr, dtype=np.int64)[None, :]
+            for c0 in range(0, n, 1 << 20):  # chunked scatter of the header rows
+                c1 = min(n, c0 + (1 << 20))
+                pos = offs[c0:c1, None] + cols
+                keep = cols < sizes[c0:c1, None]
+                umem[pos[keep]] = h[c0:c1][keep]
     descs = np.zeros(n, dtype=d_desc)
     descs["addr"] = offs
     descs["len"] = sizes
@@ -456,8 +459,7 @@ def setup_vm(vm, name: str) -> int:
         m = vm.add_map(mdef)
         if entries is not None:
             keys, vals = entries
-            for k, v in zip(keys, vals):
-                vm.map_update(m, k.tobytes(), v.tobytes())
+            vm.map_update_batch(m, keys, vals)
     prog = vm.add_raw_program(CONFIGS[name]["program"]())
     vm.set_entrypoint(prog)
     return prog

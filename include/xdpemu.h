@@ -204,6 +204,9 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
 int xe_map_lookup(xe_vm* vm, int32_t map_idx, const void* key, void* value_out);
 int xe_map_update(xe_vm* vm, int32_t map_idx, const void* key, const void* value);
 int xe_map_delete(xe_vm* vm, int32_t map_idx, const void* key);
+/* bulk form of xe_map_update (count consecutive keys / values); stops at the first failure and
+ * returns its code (the kernel-map counterpart is gobpfld's BPFMap.UpdateBatch, map.go) */
+int xe_map_update_batch(xe_vm* vm, int32_t map_idx, const void* keys, const void* values, uint64_t count);
 /* Final-state dump. ARRAY: raw ValueSize*MaxEntries bytes into `keys_or_raw`.
  * HASH: entries sorted by key bytes; keys into keys_or_raw (count*key_size), values into values
  * (count*value_size). Pass NULL buffers to query the count/byte size in *count / *bytes. */

@@ -1047,6 +1047,15 @@ int orc_map_update(orc_vm* o, int32_t mi, const void* key, const void* value) {
   return XE_OK;
 }
 
+int orc_map_update_batch(orc_vm* o, int32_t mi, const void* keys, const void* values, uint64_t count) {
+  Map* m = getMap(o, mi);
+  if (!m) return XE_ERR_INVAL;
+  const size_t ks = m->isHash() ? m->def.key_size : 4, vs = m->def.value_size;
+  for (uint64_t i = 0; i < count; i++)
+    if (int rc = orc_map_update(o, mi, (const uint8_t*)keys + i * ks, (const uint8_t*)values + i * vs)) return rc;
+  return XE_OK;
+}
+
 int orc_map_delete(orc_vm* o, int32_t mi, const void* key) {
   Map* m = getMap(o, mi);
   if (!m || !m->isHash()) return XE_ERR_INVAL;

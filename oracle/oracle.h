@@ -23,6 +23,7 @@ int orc_add_map(orc_vm* vm, const xe_map_def* def, const void* init, size_t init
 int orc_map_lookup(orc_vm* vm, int32_t map_idx, const void* key, void* value_out);
 int orc_map_update(orc_vm* vm, int32_t map_idx, const void* key, const void* value);
 int orc_map_delete(orc_vm* vm, int32_t map_idx, const void* key);
+int orc_map_update_batch(orc_vm* vm, int32_t map_idx, const void* keys, const void* values, uint64_t count);
 int orc_map_count(orc_vm* vm, int32_t map_idx, uint64_t* count);
 int orc_map_dump(orc_vm* vm, int32_t map_idx, void* keys_or_raw, void* values, uint64_t cap, uint64_t* count);
 /* Sequential per-packet harness over host memory; packet writes land in umem. */

@@ -141,6 +141,10 @@ struct XeParams {
   uint32_t ingress;
   uint32_t rxq;
   uint32_t* flags;             // XE_FLAG_*
-  unsigned long long* fp;      // [(nmaps+1)*2]: read mask, atomic mask per map
-  unsigned long long* stats;   // [0] steps, [1..8] status histogram
+  // per-wave flushes go to replica (wave % nrep) to avoid same-address atomic chains; the host
+  // reduces the replicas: record = [0] steps, [1..8] status histogram, [16 + 2m] read mask and
+  // [17 + 2m] atomic mask of map m
+  unsigned long long* rep;
+  uint32_t nrep;
+  uint32_t rep_words;
 };

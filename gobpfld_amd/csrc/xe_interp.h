@@ -151,6 +151,7 @@ struct XeLane {
   // wave-uniform batch statistics, flushed once per wave (flush_wave_state)
   uint64_t acc_steps;
   uint32_t acc_status[8];
+  unsigned long long* rep;  // this wave's statistics / footprint replica record
 };
 
 
@@ -302,7 +303,7 @@ XE_DEV void fp_record(XeLane& L, const XeParams& P, uint32_t m, bool atomic, uin
       }
     }
   } else {
-    xe_atomic_or64(&P.fp[m * 2 + (atomic ? 1 : 0)], bits);
+    xe_atomic_or64(&L.rep[16 + m * 2 + (atomic ? 1 : 0)], bits);
   }
 }
 
@@ -1143,7 +1144,8 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
 }
 
-XE_DEV void wave_state_init(XeLane& L) {
+XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave) {
+  L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
 #pragma unroll
   for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
   L.acc_steps = 0;
@@ -1198,10 +1200,10 @@ XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
   for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o);
 #endif
   if (xe_lane() == 0) {
-    if (steps) xe_atomic_add64(&P.stats[0], steps);
+    if (steps) xe_atomic_add64(&L.rep[0], steps);
 #pragma unroll
     for (int st = 0; st < 8; st++)
-      if (L.acc_status[st]) xe_atomic_add64(&P.stats[1 + st], L.acc_status[st]);
+      if (L.acc_status[st]) xe_atomic_add64(&L.rep[1 + st], L.acc_status[st]);
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1210,8 +1212,8 @@ XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
     for (int o = 32; o > 0; o >>= 1) { r |= __shfl_xor(r, o); a |= __shfl_xor(a, o); }
 #endif
     if (xe_lane() == 0) {
-      if (r) xe_atomic_or64(&P.fp[(k + 1) * 2], r);
-      if (a) xe_atomic_or64(&P.fp[(k + 1) * 2 + 1], a);
+      if (r) xe_atomic_or64(&L.rep[16 + (k + 1) * 2], r);
+      if (a) xe_atomic_or64(&L.rep[16 + (k + 1) * 2 + 1], a);
     }
   }
 }

@@ -48,7 +48,7 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   L.mem = &M;
   uint8_t hdrbuf[XE_HDR_STRIDE];
   L.hdr = hdrbuf;
-  wave_state_init(L);
+  wave_state_init(L, *P, 0);
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
     run_packet(L, *P, i, true);
@@ -339,7 +339,9 @@ struct xe_vm {
 
 namespace {
 
-constexpr size_t kAuxWords = 32 + 2 * 64;
+constexpr uint32_t kRep = 64;                  // statistics / footprint replicas
+constexpr uint32_t kRepWords = 16 + 2 * 64;      // per replica: stats + (read, atomic) per map
+constexpr size_t kAuxWords = 16 + size_t(kRep) * kRepWords;
 
 int fail(xe_vm* vm, int rc, const std::string& msg) {
   if (vm) vm->last_error = msg;
@@ -706,9 +708,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   P.max_steps = vm->settings.max_steps;
   P.ingress = vm->settings.ingress_ifindex;
   P.rxq = vm->settings.rx_queue_index;
-  P.stats = vm->d_aux;
-  P.flags = reinterpret_cast<uint32_t*>(vm->d_aux + 16);
-  P.fp = vm->d_aux + 32;
+  P.flags = reinterpret_cast<uint32_t*>(vm->d_aux);
+  P.rep = vm->d_aux + 16;
+  P.nrep = kRep;
+  P.rep_words = 16 + 2 * (P.nmaps + 1);
+  const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
 
   const uint32_t mode = vm->settings.mode;
   uint32_t engine = vm->settings.engine;
@@ -739,7 +743,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     HostMap& m = vm->maps[i];
     if (d2d(m.d_snap, m.d_vals, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "snapshot");
   }
-  if (dmemset(vm->d_aux, 0, kAuxWords * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
+  if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
   vm->t0.rec(s);
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
@@ -752,37 +756,51 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (launch(&P, grid_blocks(n), 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   }
   vm->t1.rec(s);
-  std::vector<unsigned long long> aux(kAuxWords);
-  if (d2h(aux.data(), vm->d_aux, kAuxWords * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+  std::vector<unsigned long long> aux(aux_used);
+  // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
+  auto reduce = [&](std::vector<unsigned long long>& sum) {
+    sum.assign(16 + 2 * size_t(P.nmaps + 1), 0);
+    sum[0] = aux[0];
+    for (uint32_t r = 0; r < kRep; r++) {
+      const unsigned long long* rec = aux.data() + 16 + size_t(r) * P.rep_words;
+      sum[1] += rec[0];
+      for (int k = 0; k < 8; k++) sum[2 + k] += rec[1 + k];
+      for (uint32_t w = 0; w < 2 * (P.nmaps + 1); w++) sum[16 + w] |= rec[16 + w];
+    }
+  };
+  std::vector<unsigned long long> red;
+  if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+  reduce(red);
   float kms = Timer::ms(vm->t0, vm->t1);
   if (mode != XE_MODE_SEQUENTIAL) {
-    uint32_t flags = uint32_t(aux[16]);
+    uint32_t flags = uint32_t(red[0]);
     conflict = (flags & XE_FLAG_ORDERED) != 0;
     for (uint32_t m = 1; m <= P.nmaps && m < 64; m++)
-      if (aux[32 + 2 * m] & aux[32 + 2 * m + 1]) conflict = true;
+      if (red[16 + 2 * m] & red[16 + 2 * m + 1]) conflict = true;
     if (conflict && mode == XE_MODE_AUTO) {
       // order-dependent batch: roll the maps back and replay it in packet order on one lane
       for (size_t i = 1; i < vm->maps.size(); i++) {
         HostMap& m = vm->maps[i];
         if (d2d(m.d_vals, m.d_snap, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
       }
-      if (dmemset(vm->d_aux, 0, kAuxWords * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
+      if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
       P.mode = XE_MODE_SEQUENTIAL;
       used = XE_MODE_SEQUENTIAL;
       vm->t1.rec(s);
       if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t2.rec(s);
-      if (d2h(aux.data(), vm->d_aux, kAuxWords * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+      if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+      reduce(red);
       kms += Timer::ms(vm->t1, vm->t2);
     }
   }
-  vm->last_flags = uint32_t(aux[16]);
-  vm->last_fp.assign(aux.begin() + 32, aux.end());
+  vm->last_flags = uint32_t(red[0]);
+  vm->last_fp.assign(red.begin() + 16, red.end());
   for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   if (stats) {
     stats->packets = n;
-    stats->steps = aux[0];
-    for (int k = 0; k < 8; k++) stats->status_count[k] = aux[1 + k];
+    stats->steps = red[1];
+    for (int k = 0; k < 8; k++) stats->status_count[k] = red[2 + k];
     stats->mode_used = used;
     stats->conflict = conflict ? 1 : 0;
     stats->kernel_ms = kms;

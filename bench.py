@@ -34,19 +34,37 @@ WORKLOADS = {
 }  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec peak
 
 
-def alg_bytes_per_packet(sizes: np.ndarray) -> np.ndarray:
-    """16 B descriptor + min(len, 64) header window + 4 B verdict."""
+def alg_bytes_per_packet(name: str, sizes: np.ndarray) -> np.ndarray:
+    """16 B descriptor + min(len, 64) header window + 4 B verdict (C2-C5); C1 reads no
+    packet bytes, so 16 + 4."""
+    if name == "c1":
+        return np.full(sizes.shape, 20, dtype=np.int64)
     return 16 + np.minimum(sizes, 64) + 4
 
 
-def cpu_baseline(name: str, n_sample: int) -> dict:
-    """The oracle (C++ restatement of emulator/, one thread) timed on a bounded prefix of the workload."""
+ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
+ISSUE_PEAK = 256 * 64 * 2.4e9  # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz (SURVEY §8d issue roofline)
+
+
+def cpu_baseline(name: str, n_sample: int, target_s: float = 15.0) -> dict:
+    """The oracle (C++ restatement of emulator/, one thread) timed on a bounded prefix of the workload.
+
+    n_sample = 0 calibrates on a 20k-packet prefix and then times a prefix sized for ~target_s seconds."""
     from gobpfld_amd import _native as N
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
     from gobpfld_amd import build as B
     B.build_oracle()
     vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
+    if not n_sample:
+        W.setup_vm(vm, name)
+        cu, cd = W.build_batch(name, 0, 20_000)
+        t0 = time.perf_counter()
+        vm.run_batch(cu, cd)
+        rate = 20_000 / (time.perf_counter() - t0)
+        n_sample = int(min(max(rate * target_s, 50_000), 8_000_000))
+        vm.close()
+        vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
     W.setup_vm(vm, name)
     umem, descs = W.build_batch(name, 0, n_sample)
     t0 = time.perf_counter()
@@ -145,15 +163,14 @@ def main() -> None:
     total_pkts = n * world * args.steps
     value = total_pkts / elapsed / 1e6
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
-    bytes_per_launch = float(alg_bytes_per_packet(sizes).sum())
+    bytes_per_launch = float(alg_bytes_per_packet(name, sizes).sum())
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     insns_per_pkt = steps_retired / max(1, n * args.steps)
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
-            sample = args.cpu_sample or (200_000 if name != "c4" else 100_000)
-            cpu = cpu_baseline(name, sample)
+            cpu = cpu_baseline(name, args.cpu_sample)
         hw = {"c2": "64B", "c3": "IMIX 64/576/1500B", "c4": "1500B", "c5": "64B"}.get(name, "64B")
         out = {
             "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches",
@@ -177,7 +194,8 @@ def main() -> None:
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
                          "kernel": "xe_jit_kernel" if engines == {"jit"} else "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(bytes_per_launch),
-                         "alg_bytes_per_packet": "16 desc + min(len,64) header + 4 verdict"},
+                         "alg_bytes_per_packet": ALG_DESC.get(name, "16 desc + min(len,64) header + 4 verdict"),
+                         "issue_frac": round(insns_per_pkt * n / avg_kernel_s / ISSUE_PEAK, 5)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -108,6 +108,16 @@ struct XeMem {
   uint64_t bm[XE_NWORDS];
 };
 
+// per-wave combining cache of deferred map atomics (parallel mode only), kept in LDS and touched by
+// one lane at a time (the aggregation leader)
+#define XE_PEND 8
+struct XePend {
+  unsigned long long addr[XE_PEND];
+  unsigned long long sum[XE_PEND];
+  int size[XE_PEND];
+  int next;  // round-robin victim
+};
+
 struct XeReg {
   int64_t v;   // RegisterValue.Value()
   uint32_t h;  // memory handle (pointers)
@@ -152,6 +162,7 @@ struct XeLane {
   uint64_t acc_steps;
   uint32_t acc_status[8];
   unsigned long long* rep;  // this wave's statistics / footprint replica record
+  XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
 };
 
 
@@ -437,7 +448,40 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
 // one leader lane adds the sum of its peers' addends (exact: the field add is modulo 2^(8*size), so
 // the sum of several adds equals one add of their sum). Removes same-address contention for hot
 // counters (C2's per-proto array, hot flows).
-XE_DEV void wave_atomic_add_field(uint8_t* p, int size, uint64_t add) {
+XE_DEV void pend_add(XePend* pd, uint64_t addr, int size, uint64_t sum) {
+  if (!pd) { atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(addr)), size, sum); return; }
+  // fully associative, branch-free probe: all tags are loaded at once, the hit / free / victim
+  // entry is selected in registers; a miss with no free entry evicts (applies) the victim
+  uint64_t ta[XE_PEND];
+  int ts[XE_PEND];
+#pragma unroll
+  for (int k = 0; k < XE_PEND; k++) { ta[k] = pd->addr[k]; ts[k] = pd->size[k]; }
+  int hit = -1, fr = -1;
+#pragma unroll
+  for (int k = XE_PEND - 1; k >= 0; k--) {
+    hit = (ts[k] == size && ta[k] == addr) ? k : hit;
+    fr = ts[k] == 0 ? k : fr;
+  }
+  if (hit >= 0) { pd->sum[hit] += sum; return; }
+  int k = fr;
+  if (k < 0) {
+    k = pd->next;
+    pd->next = (k + 1) & (XE_PEND - 1);
+    atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
+  }
+  pd->addr[k] = addr; pd->size[k] = size; pd->sum[k] = sum;
+}
+
+XE_DEV void pend_flush(XePend* pd) {
+  if (!pd) return;
+#pragma unroll
+  for (int k = 0; k < XE_PEND; k++) {
+    if (pd->size[k]) atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
+    pd->size[k] = 0;
+  }
+}
+
+XE_DEV void wave_atomic_add_field(XePend* pend, uint8_t* p, int size, uint64_t add) {
 #if defined(__HIPCC__)
   const uint64_t addr = uint64_t(uintptr_t(p));
   unsigned long long remaining = xe_ballot(true);
@@ -456,11 +500,12 @@ XE_DEV void wave_atomic_add_field(uint8_t* p, int size, uint64_t add) {
       sum += (uint64_t(uint32_t(xe_readlane(int(add >> 32), l))) << 32) |
              uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), l)));
     }
-    if (me == leader) atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(la)), ls, sum);
+    // a group of one gains nothing from deferral: apply it directly (fire-and-forget atomic)
+    if (me == leader) pend_add(__builtin_popcountll(peers) > 1 ? pend : nullptr, la, ls, sum);
     remaining &= ~peers;
   }
 #else
-  atomic_add_field(p, size, add);
+  pend_add(pend, uint64_t(uintptr_t(p)), size, add);
 #endif
 }
 
@@ -1005,7 +1050,8 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
   fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
-  wave_atomic_add_field(B.base + off, size, uint64_t(reg_get(L, u.src).v));
+  wave_atomic_add_field(P.mode == XE_MODE_PARALLEL ? L.pend : nullptr, B.base + off, size,
+                        uint64_t(reg_get(L, u.src).v));
   return 0;
 }
 
@@ -1144,8 +1190,14 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
 }
 
-XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave) {
+XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
   L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
+  L.pend = pend;
+  if (pend && xe_lane() == 0) {
+#pragma unroll
+    for (int k = 0; k < XE_PEND; k++) pend->size[k] = 0;
+    pend->next = 0;
+  }
 #pragma unroll
   for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
   L.acc_steps = 0;
@@ -1195,6 +1247,7 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
 // flush per-lane footprints of maps 1..4 (wave OR-reduction) and the batch statistics: one atomic
 // per word per wave
 XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
+  if (xe_lane() == 0) pend_flush(L.pend);
   unsigned long long steps = L.acc_steps;
 #if defined(__HIPCC__)
   for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o);

@@ -8,12 +8,13 @@
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[256 * XE_HDR_STRIDE];
+  __shared__ XePend pend_lds[4];
   XeMem M;
   XeLane L;
   L.mem = &M;
   L.hdr = hdr_lds + threadIdx.x * XE_HDR_STRIDE;
   const int lane = xe_lane();
-  wave_state_init(L, P, (blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  wave_state_init(L, P, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, &pend_lds[threadIdx.x >> 6]);
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
     for (uint32_t i = 0; i < P.n; i++) run_packet(L, P, i, lane == 0);

@@ -48,7 +48,8 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   L.mem = &M;
   uint8_t hdrbuf[XE_HDR_STRIDE];
   L.hdr = hdrbuf;
-  wave_state_init(L, *P, 0);
+  XePend pend;
+  wave_state_init(L, *P, 0, P->mode == XE_MODE_PARALLEL ? &pend : nullptr);
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
     run_packet(L, *P, i, true);
@@ -323,6 +324,7 @@ struct xe_vm {
   unsigned long long* d_aux = nullptr;  // [0..15] stats, [16] flags, [32..] footprints
   // host-run staging
   void* d_umem = nullptr; size_t d_umem_cap = 0;
+  void* d_usnap = nullptr; size_t d_usnap_cap = 0;  // packet bytes before a replayable parallel pass
   void* d_desc = nullptr; size_t d_desc_cap = 0;
   void* d_res = nullptr; size_t d_res_cap = 0;
   void* d_ver = nullptr; size_t d_ver_cap = 0;
@@ -501,6 +503,7 @@ void xe_destroy(xe_vm* vm) {
   for (auto& m : vm->maps) map_free_device(m);
   dev_free(vm->d_prog); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
+  dev_free(vm->d_usnap);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
 #ifndef XE_HOSTSIM
   if (vm->stream) (void)hipStreamDestroy(vm->stream);
@@ -685,6 +688,14 @@ int xe_map_dump(xe_vm* vm, int32_t mi, void* keys_or_raw, void* values, uint64_t
   return XE_OK;
 }
 
+// Can the program write packet memory? Only stores/atomics whose base is not R10 can (R10 is always
+// the frame pointer: Registers.Assign refuses it, emulator/registers.go:141-143).
+static bool may_write_packet(const std::vector<XeUop>& prog) {
+  for (const XeUop& u : prog)
+    if ((u.cls == U_ST || u.cls == U_STX || u.cls == U_ATOMIC) && u.dst != 10) return true;
+  return false;
+}
+
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
@@ -743,6 +754,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     HostMap& m = vm->maps[i];
     if (d2d(m.d_snap, m.d_vals, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "snapshot");
   }
+  // the ordered replay must also start from the original packet bytes
+  const bool keep_pkts = mode == XE_MODE_AUTO && umem_len && may_write_packet(vm->programs[vm->entry]);
+  if (keep_pkts && (ensure_buf(&vm->d_usnap, &vm->d_usnap_cap, umem_len) || d2d(vm->d_usnap, d_umem, umem_len, s)))
+    return fail(vm, XE_ERR_DEVICE, "packet snapshot");
   if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
   vm->t0.rec(s);
   bool conflict = false;
@@ -783,6 +798,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         HostMap& m = vm->maps[i];
         if (d2d(m.d_vals, m.d_snap, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
       }
+      if (keep_pkts && d2d(d_umem, vm->d_usnap, umem_len, s)) return fail(vm, XE_ERR_DEVICE, "packet rollback");
       if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
       P.mode = XE_MODE_SEQUENTIAL;
       used = XE_MODE_SEQUENTIAL;

@@ -446,6 +446,18 @@ def _(a):
     a.label("out").mov64(0, -1).exit()
 
 
+@kat("ordered_replay_restores_packet", (OK, None), maps=[ARRAY8],
+     cite="packet write (inst_store.go on ByteMemory) in an order-dependent batch: written once")
+def _(a):
+    a.ldx(4, 2, 1, 0)                                                  # r2 = data
+    a.ldx(4, 3, 2, 4).add64(3, 7).stx(4, 2, 4, 3)                      # pkt[4..8] += 7
+    a.st(4, 10, -4, 0).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "out", imm=0)
+    a.ldx(8, 1, 0, 0).mov64(6, src=1).add64(1, 1).stx(8, 0, 0, 1)    # counter++ (conflict)
+    a.mov64(0, src=6).exit()
+    a.label("out").mov64(0, -1).exit()
+
+
 @kat("xadd_then_read_conflict", (OK, None), maps=[ARRAY8], cite="atomic and read of the same bytes: order-dependent")
 def _(a):
     a.st(4, 10, -4, 1).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)

@@ -120,3 +120,18 @@ def test_c2_full_size_properties(gpu_lib):
     torch.cuda.synchronize()
     assert (np.frombuffer(vm.map_dump(1), dtype=np.uint64) == 2 * counts).all()
     vm.close()
+
+
+@pytest.mark.parametrize("engine,count", [(ENGINE_INTERP, 240), (ENGINE_JIT, 48)], ids=ENGINE_IDS)
+def test_fuzz_device_equals_oracle(gpu_lib, oracle_lib, engine, count):
+    """Random programs (tests/fuzz.py): device == oracle on every observable, per engine."""
+    from fuzz import gen_program
+    from test_fuzz_cpu import fuzz_packets
+    for seed in range(count):
+        prog, maps, entries, settings = gen_program(seed, 24 + seed % 64)
+        umem, descs = fuzz_packets(seed, 64)
+        settings.engine = engine
+        b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, settings=settings)
+        a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=settings)
+        assert a[0].stats["engine_used"] == engine
+        assert_same(a, b, f"fuzz seed {seed}")

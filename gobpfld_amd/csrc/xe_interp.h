@@ -34,15 +34,34 @@ XE_DEV unsigned long long xe_ballot(bool p) { return __ballot(p); }
 XE_DEV int xe_readfirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 XE_DEV int xe_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 XE_DEV int xe_lane() { return __lane_id(); }
-XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return atomicAdd(p, v); }
-XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { return atomicCAS(p, c, v); }
-XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { atomicOr(p, v); }
-XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) { atomicOr(p, v); }
-XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return atomicAdd(p, v); }
-XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// Global-memory pointers (packets, maps, replicas, flags) reach the kernel through memory, so the
+// compiler sees generic pointers and would emit flat instructions; XE_GP casts them to the global
+// address space (global_load / global_atomic, vmcnt-only waits).
+#define XE_GP(T) __attribute__((address_space(1))) T*
+XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_add((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) {
+  __hip_atomic_compare_exchange_strong((XE_GP(unsigned int))p, &c, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return c;
+}
+XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) {
+  __hip_atomic_fetch_or((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_fetch_or((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) {
+  return __hip_atomic_fetch_add((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) {
+  return __hip_atomic_load((XE_GP(unsigned int))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #else
 #define XE_DEV static inline
 #define XE_WAVE 1
+#define XE_GP(T) T*
 XE_DEV unsigned long long xe_ballot(bool p) { return p ? 1ull : 0ull; }
 XE_DEV int xe_readfirst(int v) { return v; }
 XE_DEV int xe_readlane(int v, int) { return v; }
@@ -337,7 +356,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   }
   uint32_t slot = xe_h_slot(h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
-  B.len = (M.state[slot] & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
+  B.len = (((XE_GP(const uint32_t))M.state)[slot] & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
   B.array = false;
   return true;
 }
@@ -349,14 +368,15 @@ XE_DEV int bounds(int64_t off, int64_t size, int64_t len) {
   return 0;
 }
 
-XE_DEV uint64_t load_le(const uint8_t* p, int size) {
-  uintptr_t a = uintptr_t(p);
+XE_DEV uint64_t load_le(const uint8_t* p0, int size) {
+  XE_GP(const uint8_t) p = (XE_GP(const uint8_t))p0;
+  uintptr_t a = uintptr_t(p0);
   if ((a & uintptr_t(size - 1)) == 0) {
     switch (size) {
       case 1: return *p;
-      case 2: return *reinterpret_cast<const uint16_t*>(p);
-      case 4: return *reinterpret_cast<const uint32_t*>(p);
-      default: return *reinterpret_cast<const uint64_t*>(p);
+      case 2: return *(XE_GP(const uint16_t))p;
+      case 4: return *(XE_GP(const uint32_t))p;
+      default: return *(XE_GP(const uint64_t))p;
     }
   }
   uint64_t x = 0;
@@ -365,14 +385,15 @@ XE_DEV uint64_t load_le(const uint8_t* p, int size) {
   return x;
 }
 
-XE_DEV void store_le(uint8_t* p, int size, uint64_t x) {
-  uintptr_t a = uintptr_t(p);
+XE_DEV void store_le(uint8_t* p0, int size, uint64_t x) {
+  XE_GP(uint8_t) p = (XE_GP(uint8_t))p0;
+  uintptr_t a = uintptr_t(p0);
   if ((a & uintptr_t(size - 1)) == 0) {
     switch (size) {
       case 1: *p = uint8_t(x); return;
-      case 2: *reinterpret_cast<uint16_t*>(p) = uint16_t(x); return;
-      case 4: *reinterpret_cast<uint32_t*>(p) = uint32_t(x); return;
-      default: *reinterpret_cast<uint64_t*>(p) = x; return;
+      case 2: *(XE_GP(uint16_t))p = uint16_t(x); return;
+      case 4: *(XE_GP(uint32_t))p = uint32_t(x); return;
+      default: *(XE_GP(uint64_t))p = x; return;
     }
   }
 #pragma unroll 1
@@ -429,7 +450,7 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
     uint64_t part = (consumed < 8 ? (add >> (8 * consumed)) : 0) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1ull));
     uint64_t addend = part + carry;  // may exceed the slice width by one carry bit
     unsigned int* wp = reinterpret_cast<unsigned int*>(w);
-    unsigned int old = *wp, assumed;
+    unsigned int old = *(XE_GP(unsigned int))wp, assumed;
     uint64_t sum;
     do {
       assumed = old;
@@ -448,23 +469,43 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
 // one leader lane adds the sum of its peers' addends (exact: the field add is modulo 2^(8*size), so
 // the sum of several adds equals one add of their sum). Removes same-address contention for hot
 // counters (C2's per-proto array, hot flows).
+// XE_PEND_MODE: 0 = apply immediately, 1 = fully associative branch-free probe, 2 = early-exit probe
+#ifndef XE_PEND_MODE
+#define XE_PEND_MODE 1
+#endif
+#ifndef XE_SINGLE_BYPASS
+#define XE_SINGLE_BYPASS 1
+#endif
+#ifndef XE_UNIFORM_SUM
+#define XE_UNIFORM_SUM 1
+#endif
+
+// pd is never selected against null (that would turn the LDS pointer generic: flat instructions)
 XE_DEV void pend_add(XePend* pd, uint64_t addr, int size, uint64_t sum) {
-  if (!pd) { atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(addr)), size, sum); return; }
-  // fully associative, branch-free probe: all tags are loaded at once, the hit / free / victim
-  // entry is selected in registers; a miss with no free entry evicts (applies) the victim
-  uint64_t ta[XE_PEND];
-  int ts[XE_PEND];
-#pragma unroll
-  for (int k = 0; k < XE_PEND; k++) { ta[k] = pd->addr[k]; ts[k] = pd->size[k]; }
+  if (XE_PEND_MODE == 0) { atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(addr)), size, sum); return; }
   int hit = -1, fr = -1;
+  if (XE_PEND_MODE == 2) {
 #pragma unroll
-  for (int k = XE_PEND - 1; k >= 0; k--) {
-    hit = (ts[k] == size && ta[k] == addr) ? k : hit;
-    fr = ts[k] == 0 ? k : fr;
+    for (int k = 0; k < XE_PEND; k++) {
+      const int ts = pd->size[k];
+      if (ts == size && pd->addr[k] == addr) { hit = k; break; }
+      if (ts == 0) { fr = k; break; }
+    }
+  } else {
+    // all tags are loaded at once; the hit / free entry is selected in registers
+    uint64_t ta[XE_PEND];
+    int ts[XE_PEND];
+#pragma unroll
+    for (int k = 0; k < XE_PEND; k++) { ta[k] = pd->addr[k]; ts[k] = pd->size[k]; }
+#pragma unroll
+    for (int k = XE_PEND - 1; k >= 0; k--) {
+      hit = (ts[k] == size && ta[k] == addr) ? k : hit;
+      fr = ts[k] == 0 ? k : fr;
+    }
   }
   if (hit >= 0) { pd->sum[hit] += sum; return; }
   int k = fr;
-  if (k < 0) {
+  if (k < 0) {  // full: evict (apply) a round-robin victim
     k = pd->next;
     pd->next = (k + 1) & (XE_PEND - 1);
     atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
@@ -473,7 +514,6 @@ XE_DEV void pend_add(XePend* pd, uint64_t addr, int size, uint64_t sum) {
 }
 
 XE_DEV void pend_flush(XePend* pd) {
-  if (!pd) return;
 #pragma unroll
   for (int k = 0; k < XE_PEND; k++) {
     if (pd->size[k]) atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
@@ -481,11 +521,19 @@ XE_DEV void pend_flush(XePend* pd) {
   }
 }
 
-XE_DEV void wave_atomic_add_field(XePend* pend, uint8_t* p, int size, uint64_t add) {
+XE_DEV void wave_atomic_add_field(XePend* pend, bool defer, uint8_t* p, int size, uint64_t add) {
 #if defined(__HIPCC__)
   const uint64_t addr = uint64_t(uintptr_t(p));
   unsigned long long remaining = xe_ballot(true);
   const int me = xe_lane();
+  // parallel pre-probe: every active lane looks its field up in the wave's cache at once (broadcast
+  // LDS reads), so a group of one whose counter is already cached (e.g. the hot counter reached from
+  // a rare parse path) still accumulates locally, while unique addresses skip the LDS entirely
+  int hk = -1;
+  if (defer) {
+#pragma unroll
+    for (int k = XE_PEND - 1; k >= 0; k--) hk = (pend->size[k] == size && pend->addr[k] == addr) ? k : hk;
+  }
   while (remaining) {
     const int leader = __builtin_ctzll(remaining);
     const uint64_t la = (uint64_t(uint32_t(xe_readlane(int(addr >> 32), leader))) << 32) |
@@ -494,18 +542,33 @@ XE_DEV void wave_atomic_add_field(XePend* pend, uint8_t* p, int size, uint64_t a
     const unsigned long long peers = xe_ballot(addr == la && size == ls) & remaining;
     uint64_t sum = 0;
     unsigned long long m = peers;
+    if (XE_UNIFORM_SUM) {  // counters: every peer adds the same amount
+      const uint64_t lv = (uint64_t(uint32_t(xe_readlane(int(add >> 32), leader))) << 32) |
+                          uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), leader)));
+      if ((xe_ballot(add == lv) & peers) == peers) {
+        sum = lv * uint64_t(__builtin_popcountll(peers));
+        m = 0;
+      }
+    }
     while (m) {
       const int l = __builtin_ctzll(m);
       m &= m - 1;
       sum += (uint64_t(uint32_t(xe_readlane(int(add >> 32), l))) << 32) |
              uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), l)));
     }
-    // a group of one gains nothing from deferral: apply it directly (fire-and-forget atomic)
-    if (me == leader) pend_add(__builtin_popcountll(peers) > 1 ? pend : nullptr, la, ls, sum);
+    // cached field: accumulate (re-checked: an insert earlier in this loop may have evicted it);
+    // an uncached group of one gains nothing from deferral: apply it directly (fire-and-forget)
+    const int lhk = xe_readlane(hk, leader);
+    if (me == leader) {
+      if (defer && lhk >= 0 && pend->addr[lhk] == la && pend->size[lhk] == ls) pend->sum[lhk] += sum;
+      else if (defer && (!XE_SINGLE_BYPASS || __builtin_popcountll(peers) > 1)) pend_add(pend, la, ls, sum);
+      else atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(la)), ls, sum);
+    }
     remaining &= ~peers;
   }
 #else
-  pend_add(pend, uint64_t(uintptr_t(p)), size, add);
+  if (defer) pend_add(pend, uint64_t(uintptr_t(p)), size, add);
+  else atomic_add_field(p, size, add);
 #endif
 }
 
@@ -654,21 +717,22 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
   if (count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
 #pragma unroll 1
-  for (int64_t i = 0; i < count; i++) emit(i, B.base[off + i]);
+  for (int64_t i = 0; i < count; i++) emit(i, ((XE_GP(const uint8_t))B.base)[off + i]);
   return 0;
 }
 
 // ------------------------------------------------------------------ hash map
 XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
-  if (empty) return (M.state[M.cap] & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
+  XE_GP(const uint32_t) state = (XE_GP(const uint32_t))M.state;
+  if (empty) return (state[M.cap] & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
   uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(hv) & mask;
 #pragma unroll 1
   for (uint32_t probe = 0; probe < M.cap; probe++) {
-    uint32_t st = M.state[idx];
+    uint32_t st = state[idx];
     if (!(st & XE_SLOT_FULL)) return -1;
-    const uint64_t* k = M.keys + uint64_t(idx) * M.kwords;
+    XE_GP(const uint64_t) k = (XE_GP(const uint64_t))M.keys + uint64_t(idx) * M.kwords;
     bool eq = true;
 #pragma unroll 1
     for (uint32_t w = 0; w < M.kwords; w++) eq = eq && (k[w] == kw[w]);
@@ -1050,8 +1114,7 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
   fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
-  wave_atomic_add_field(P.mode == XE_MODE_PARALLEL ? L.pend : nullptr, B.base + off, size,
-                        uint64_t(reg_get(L, u.src).v));
+  wave_atomic_add_field(L.pend, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
   return 0;
 }
 
@@ -1193,7 +1256,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
   L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
   L.pend = pend;
-  if (pend && xe_lane() == 0) {
+  if (xe_lane() == 0) {
 #pragma unroll
     for (int k = 0; k < XE_PEND; k++) pend->size[k] = 0;
     pend->next = 0;

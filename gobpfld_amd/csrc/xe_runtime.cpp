@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <array>
 #include <vector>
 
 #ifdef XE_HOSTSIM
@@ -49,7 +50,7 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   uint8_t hdrbuf[XE_HDR_STRIDE];
   L.hdr = hdrbuf;
   XePend pend;
-  wave_state_init(L, *P, 0, P->mode == XE_MODE_PARALLEL ? &pend : nullptr);
+  wave_state_init(L, *P, 0, &pend);
   for (uint32_t i = 0; i < P->n; i++) {
     if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
     run_packet(L, *P, i, true);
@@ -321,6 +322,7 @@ struct xe_vm {
   size_t d_prog_len = 0;
   XeDevMap* d_maps = nullptr;
   size_t d_maps_n = 0;
+  std::vector<XeDevMap> dm_uploaded;  // host copy of the device map table (upload only on change)
   unsigned long long* d_aux = nullptr;  // [0..15] stats, [16] flags, [32..] footprints
   // host-run staging
   void* d_umem = nullptr; size_t d_umem_cap = 0;
@@ -406,7 +408,7 @@ HostMap* get_map(xe_vm* vm, int32_t idx) {
   return &vm->maps[idx];
 }
 
-int prepare_run(xe_vm* vm) {
+int prepare_run(xe_vm* vm, xe_stream_t s) {
   if (vm->entry < 1 || vm->entry >= int32_t(vm->programs.size()))
     return fail(vm, XE_ERR_INVAL, "no program loaded at PI");
   if (set_device(vm->settings.device)) return fail(vm, XE_ERR_DEVICE, "hipSetDevice failed");
@@ -416,7 +418,7 @@ int prepare_run(xe_vm* vm) {
     vm->d_prog = nullptr;
     if (dev_alloc((void**)&vm->d_prog, std::max<size_t>(prog.size(), 1) * sizeof(XeUop)))
       return fail(vm, XE_ERR_DEVICE, "device alloc (program)");
-    if (!prog.empty() && h2d(vm->d_prog, prog.data(), prog.size() * sizeof(XeUop), vm->stream))
+    if (!prog.empty() && (h2d(vm->d_prog, prog.data(), prog.size() * sizeof(XeUop), vm->stream) || dsync(vm->stream)))
       return fail(vm, XE_ERR_DEVICE, "program upload");
     vm->d_prog_idx = vm->entry;
     vm->d_prog_len = prog.size();
@@ -448,7 +450,11 @@ int prepare_run(xe_vm* vm) {
     if (dev_alloc((void**)&vm->d_maps, dm.size() * sizeof(XeDevMap))) return fail(vm, XE_ERR_DEVICE, "device alloc (maps)");
     vm->d_maps_n = dm.size();
   }
-  if (h2d(vm->d_maps, dm.data(), dm.size() * sizeof(XeDevMap), vm->stream)) return fail(vm, XE_ERR_DEVICE, "map table upload");
+  if (vm->dm_uploaded.size() != dm.size() || memcmp(vm->dm_uploaded.data(), dm.data(), dm.size() * sizeof(XeDevMap))) {
+    if (h2d(vm->d_maps, dm.data(), dm.size() * sizeof(XeDevMap), s) || dsync(s))
+      return fail(vm, XE_ERR_DEVICE, "map table upload");
+    vm->dm_uploaded = dm;
+  }
   if (!vm->d_aux && dev_alloc((void**)&vm->d_aux, kAuxWords * 8)) return fail(vm, XE_ERR_DEVICE, "device alloc (aux)");
   return XE_OK;
 }
@@ -688,20 +694,77 @@ int xe_map_dump(xe_vm* vm, int32_t mi, void* keys_or_raw, void* values, uint64_t
   return XE_OK;
 }
 
-// Can the program write packet memory? Only stores/atomics whose base is not R10 can (R10 is always
-// the frame pointer: Registers.Assign refuses it, emulator/registers.go:141-143).
+// Can the program write packet memory? A conservative may-point-to analysis over the micro-op CFG:
+// per register the bits PKT (may hold a packet pointer), CTX and FRM (ValueMemory-backed pointers),
+// plus one flow-insensitive set of what may have been spilled into ValueMemory (stack/ctx hold
+// pointer objects, emulator/memory.go:23-30). Packet pointers originate in ctx loads
+// (the xdp_md data/data_end fields); map values are ByteMemory and only ever yield scalars.
 static bool may_write_packet(const std::vector<XeUop>& prog) {
-  for (const XeUop& u : prog)
-    if ((u.cls == U_ST || u.cls == U_STX || u.cls == U_ATOMIC) && u.dst != 10) return true;
-  return false;
+  enum : uint8_t { T_PKT = 1, T_CTX = 2, T_FRM = 4 };
+  const size_t n = prog.size();
+  if (!n) return false;
+  std::vector<std::array<uint8_t, 11>> in(n);
+  std::vector<bool> reach(n, false);
+  std::array<uint8_t, 11> entry{};
+  entry[1] = T_CTX;
+  entry[10] = T_FRM;
+  uint8_t spilled = 0;
+  for (int round = 0; round < 64; round++) {
+    for (auto& r : in) r.fill(0);
+    std::fill(reach.begin(), reach.end(), false);
+    in[0] = entry;
+    reach[0] = true;
+    const uint8_t spilled0 = spilled;
+    bool changed = true;
+    while (changed) {
+      changed = false;
+      for (size_t pc = 0; pc < n; pc++) {
+        if (!reach[pc]) continue;
+        const XeUop& u = prog[pc];
+        std::array<uint8_t, 11> r = in[pc];
+        auto reg = [&](int x) -> uint8_t { return x <= 10 ? r[x] : 0; };
+        auto set = [&](int x, uint8_t v) { if (x <= 10) r[x] = v; };
+        int succ[2] = {int(pc) + 1, -1};
+        switch (u.cls) {
+          case U_FAIL: case U_EXIT: succ[0] = -1; break;
+          case U_CALLBPF: case U_CALLX: return true;  // not analysed: be conservative
+          case U_JA: succ[0] = u.tgt + 1; break;
+          case U_JMP: succ[1] = u.tgt + 1; break;
+          case U_MOVI: set(u.dst, 0); break;
+          case U_MOVR: set(u.dst, reg(u.src)); break;
+          case U_ALU: set(u.dst, uint8_t(reg(u.dst) | ((u.fl & UF_REG) ? reg(u.src) : 0))); break;
+          case U_LDX: {
+            const uint8_t s = reg(u.src);
+            set(u.dst, uint8_t(((s & T_CTX) ? T_PKT : 0) | ((s & (T_CTX | T_FRM)) ? spilled : 0)));
+            break;
+          }
+          case U_ST: case U_STX: case U_ATOMIC:
+            if (reg(u.dst) & T_PKT) return true;
+            if (u.cls == U_STX && (reg(u.dst) & (T_CTX | T_FRM))) spilled |= reg(u.src);
+            break;
+          case U_HELPER: set(0, 0); break;  // R0 := map value pointer or scalar
+          default: break;                   // NOP, NEG, END, LDIMM64 (in place: taint kept)
+        }
+        for (int k = 0; k < 2; k++) {
+          const int t = succ[k];
+          if (t < 0 || t >= int(n)) continue;
+          std::array<uint8_t, 11> m = in[t];
+          for (int x = 0; x <= 10; x++) m[x] |= r[x];
+          if (!reach[t] || m != in[t]) { in[t] = m; reach[t] = true; changed = true; }
+        }
+      }
+    }
+    if (spilled == spilled0) return false;  // fixed point including the spill set
+  }
+  return true;
 }
 
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
   if (stats) memset(stats, 0, sizeof *stats);
-  if (int rc = prepare_run(vm)) return rc;
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (int rc = prepare_run(vm, s)) return rc;
   if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
 
   XeParams P{};
@@ -901,6 +964,15 @@ int xe_translate_uops(const uint64_t* insns, uint32_t n, void* out, uint32_t cap
   if (rc) return rc;
   if (out && cap >= prog.size()) memcpy(out, prog.data(), prog.size() * sizeof(XeUop));
   return int(prog.size());
+}
+
+// debug: 1 if the translated program may write packet memory (drives the replay's packet snapshot)
+int xe_debug_may_write_packet(const uint64_t* insns, uint32_t n) {
+  std::vector<XeUop> prog;
+  std::string err;
+  int rc = translate(insns, n, prog, err);
+  if (rc) return rc;
+  return may_write_packet(prog) ? 1 : 0;
 }
 
 const char* xe_version(void) {

@@ -43,3 +43,32 @@ def test_fuzz_hostsim_equals_oracle(oracle_lib, hostsim_lib, block):
         statuses += np.bincount(b[0].results["status"], minlength=8)[:8]
     # the generator must reach normal exits and error paths alike
     assert statuses[0] > 0 and statuses[1] > 0, statuses
+
+
+def _may_write(lib, prog):
+    import ctypes as C
+    arr = np.ascontiguousarray(np.asarray(prog, dtype=np.uint64))
+    fn = lib.dll.xe_debug_may_write_packet
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_void_p, C.c_uint32]
+    return fn(arr.ctypes.data, len(arr))
+
+
+def test_packet_write_analysis_is_sound(oracle_lib, hostsim_lib):
+    """Programs the analysis clears never change packet bytes in the oracle; the configs are cleared."""
+    from gobpfld_amd import workloads as W
+    for name in ("c1", "c2", "c3", "c4", "c5"):
+        assert _may_write(hostsim_lib, W.CONFIGS[name]["program"]()) == 0, name
+    cleared = flagged = 0
+    for seed in range(600):
+        prog, maps, entries, settings = gen_program(seed)
+        umem, descs = fuzz_packets(seed)
+        verdict = _may_write(hostsim_lib, prog)
+        assert verdict in (0, 1)
+        b, _ = _try(oracle_lib, prog, maps, entries, umem, descs, settings)
+        if verdict == 0:
+            cleared += 1
+            assert np.array_equal(b[2], umem), f"seed {seed}: packet written but analysis cleared it"
+        else:
+            flagged += 1
+    assert cleared > 50 and flagged > 50, (cleared, flagged)

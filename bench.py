@@ -140,7 +140,7 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    kernel_ms, mode, conflicts, steps_retired, status_ok, engines = [], set(), 0, 0, 0, set()
+    kernel_ms, mode, conflicts, steps_retired, status_ok, engines, grid = [], set(), 0, 0, 0, set(), 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
@@ -150,6 +150,7 @@ def main() -> None:
         conflicts += st["conflict"]
         steps_retired += st["steps"]
         status_ok += st["status_count"][0]
+        grid = st["grid_blocks"]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -189,7 +190,8 @@ def main() -> None:
                        "packets_per_gpu": n, "packet_size": hw, "parallelism": f"dp{world} (packet shards)",
                        "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
                        "engine": sorted(engines),
-                       "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps)},
+                       "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps),
+                       "grid": grid},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
                          "kernel": "xe_jit_kernel" if engines == {"jit"} else "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),

@@ -42,7 +42,7 @@ class Settings(C.Structure):  # emulator/vm.go:282-296 + device knobs
 class BatchStats(C.Structure):
     _fields_ = [("packets", C.c_uint64), ("steps", C.c_uint64), ("status_count", C.c_uint64 * 8),
                 ("mode_used", C.c_uint32), ("conflict", C.c_uint32), ("kernel_ms", C.c_float),
-                ("total_ms", C.c_float), ("engine_used", C.c_uint32), ("reserved", C.c_uint32)]
+                ("total_ms", C.c_float), ("engine_used", C.c_uint32), ("grid_blocks", C.c_uint32)]
 
 
 # numpy dtypes matching the structs (for zero-copy batch buffers)

@@ -30,14 +30,18 @@
 #if defined(__HIPCC__)
 #define XE_DEV __device__ __forceinline__
 #define XE_WAVE 64
+typedef unsigned int xe_u4 __attribute__((ext_vector_type(4)));
 XE_DEV unsigned long long xe_ballot(bool p) { return __ballot(p); }
 XE_DEV int xe_readfirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 XE_DEV int xe_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 XE_DEV int xe_lane() { return __lane_id(); }
+// force a loaded value to be materialised at this point (its s_waitcnt lands here)
+XE_DEV void xe_pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
 // Global-memory pointers (packets, maps, replicas, flags) reach the kernel through memory, so the
 // compiler sees generic pointers and would emit flat instructions; XE_GP casts them to the global
 // address space (global_load / global_atomic, vmcnt-only waits).
 #define XE_GP(T) __attribute__((address_space(1))) T*
+#define XE_LP(T) __attribute__((address_space(3))) T*
 XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) {
   return __hip_atomic_fetch_add((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -61,11 +65,17 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) {
 #else
 #define XE_DEV static inline
 #define XE_WAVE 1
+struct xe_u4 {
+  unsigned int v[4];
+  unsigned int operator[](int k) const { return v[k]; }
+};
 #define XE_GP(T) T*
+#define XE_LP(T) T*
 XE_DEV unsigned long long xe_ballot(bool p) { return p ? 1ull : 0ull; }
 XE_DEV int xe_readfirst(int v) { return v; }
 XE_DEV int xe_readlane(int v, int) { return v; }
 XE_DEV int xe_lane() { return 0; }
+XE_DEV void xe_pin(uint64_t&) {}
 XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { __atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); return c; }
 XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
@@ -83,9 +93,17 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_HAS_HASH 1
 #endif
 
-// packet header window staged in LDS per lane (the first 64 bytes are the hot bytes)
+// Packet header window staged in LDS per lane (the first 64 bytes are the hot bytes).
+// The window is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR destination) from the 16-byte
+// aligned address below the packet start, as XE_HDR_ROWS rows of 16 bytes per lane; one DMA
+// instruction writes one row for the whole wave, lane-linear (row k of lane l at k * XE_HDR_ROW +
+// l * 16). A lane's logical byte b lives at physical byte b + hsh (hsh = addr & 15) of its rows.
+// Two such buffers per wave: the next chunk's window is in flight while the current one executes.
 #define XE_HDR_WIN 64
-#define XE_HDR_STRIDE 68  // 17 dwords: lanes reading the same offset hit distinct banks
+#define XE_HDR_ROWS 5                              // 64 bytes + up to 15 bytes of misalignment
+#define XE_HDR_ROW (XE_WAVE * 16)                  // bytes of one row for the whole wave
+#define XE_HDR_BUF (XE_HDR_ROWS * XE_HDR_ROW)      // one buffer
+#define XE_HDR_WAVE_BYTES (2 * XE_HDR_BUF)         // double buffer per wave
 
 // kernel-internal error encoding
 #define XE_EV_PANIC 0x1000
@@ -118,14 +136,30 @@ XE_DEV uint64_t xe_ctx_default_word(int w) {
        : 0x0606060605050505ull;
 }
 
-// per-lane memory in scratch: object table (ids 1..63; 1..6 are the xdp_md ctx objects,
-// materialised lazily) and the ValueMemory byte maps (object ids), reset lazily via XeLane::dirty
+// Per-lane memory: object table (ids 1..63; 1..6 are the xdp_md ctx objects, materialised lazily)
+// and the ValueMemory byte maps (object ids), reset lazily via XeLane::dirty. Accessed only through
+// the xm_* functions below. The interpreter keeps them in scratch (dynamic indices); a per-program
+// kernel whose accesses are statically indexed defines XE_MEM_FIELDS and supplies XeMem as named
+// fields with switch accessors (xe_jit.cpp), so the whole table lives in VGPRs after SROA.
+#if !defined(XE_MEM_FIELDS)
+#define XE_OBJ_LIMIT XE_NOBJ
 struct XeMem {
   int64_t ov[XE_NOBJ];
   uint32_t oh[XE_NOBJ];
   uint32_t ot[XE_NOBJ];
   uint64_t bm[XE_NWORDS];
 };
+XE_DEV int64_t xm_ov(const XeMem& M, int i) { return M.ov[i]; }
+XE_DEV uint32_t xm_oh(const XeMem& M, int i) { return M.oh[i]; }
+XE_DEV uint32_t xm_ot(const XeMem& M, int i) { return M.ot[i]; }
+XE_DEV void xm_set_obj(XeMem& M, int i, int64_t v, uint32_t h, uint32_t t) { M.ov[i] = v; M.oh[i] = h; M.ot[i] = t; }
+XE_DEV void xm_set_ov(XeMem& M, int i, int64_t v) { M.ov[i] = v; }
+XE_DEV uint64_t xm_bm(const XeMem& M, int w) { return M.bm[w]; }
+XE_DEV void xm_set_bm(XeMem& M, int w, uint64_t v) { M.bm[w] = v; }
+#define XE_UNROLL_VM _Pragma("unroll 1")
+#else
+#define XE_UNROLL_VM _Pragma("unroll")
+#endif
 
 // per-wave combining cache of deferred map atomics (parallel mode only), kept in LDS and touched by
 // one lane at a time (the aggregation leader)
@@ -170,8 +204,11 @@ struct XeLane {
   // packet
   uint8_t* pkt;
   int64_t plen;
-  uint8_t* hdr;      // LDS copy of the first min(plen, 64) packet bytes
-  int32_t hdr_len;
+  XE_LP(uint8_t) hdr;      // this lane's column of the current LDS header buffer (+ lane * 16)
+  XE_LP(uint8_t) hdrbuf;   // the wave's two header buffers (wave-uniform)
+  XE_LP(const XeDevMap) maps;  // map descriptor table (LDS copy of P.maps, stage_maps)
+  int32_t hdr_len;         // min(plen, 64): bytes served from the window
+  int32_t hsh;             // physical offset of logical byte 0 in the lane's rows
   // per-lane map footprints for maps 1..4 (others go straight to global)
   uint64_t fpr[4];
   uint64_t fpa[4];
@@ -223,15 +260,13 @@ XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& 
     v = id == 2 ? L.plen : id == 4 ? int64_t(L.ingress) : id == 5 ? int64_t(L.rxq) : 0;
     return;
   }
-  v = L.mem->ov[id];
-  h = L.mem->oh[id];
-  t = L.mem->ot[id];
+  v = xm_ov(*L.mem, id);
+  h = xm_oh(*L.mem, id);
+  t = xm_ot(*L.mem, id);
 }
 
 XE_DEV void obj_set(XeLane& L, int id, int64_t v, uint32_t h, uint32_t t) {
-  L.mem->ov[id] = v;
-  L.mem->oh[id] = h;
-  L.mem->ot[id] = t;
+  xm_set_obj(*L.mem, id, v, h, t);
   L.odef &= ~(1ull << id);
 }
 
@@ -242,20 +277,22 @@ XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
     obj_get(L, id, ov, oh, ot);
     obj_set(L, id, v, oh, ot);
   } else {
-    L.mem->ov[id] = v;
+    xm_set_ov(*L.mem, id, v);
   }
 }
 
 XE_DEV uint64_t bm_word(const XeLane& L, int w) {
-  if ((L.dirty >> w) & 1ull) return L.mem->bm[w];
+  if ((L.dirty >> w) & 1ull) return xm_bm(*L.mem, w);
   return w >= XE_CTX_WORD0 ? xe_ctx_default_word(w) : 0ull;
 }
 XE_DEV void bm_set_word(XeLane& L, int w, uint64_t v) {
-  L.mem->bm[w] = v;
+  xm_set_bm(*L.mem, w, v);
   L.dirty |= 1ull << w;
 }
 
-// mark-sweep collection of object ids when the table is full
+// mark-sweep collection of object ids when the table is full (a per-program kernel with the table in
+// registers is only built when no path can fill it: XE_OBJ_LIMIT >= 7 + stores on the longest path)
+#if !defined(XE_MEM_FIELDS)
 XE_DEV void obj_gc(XeLane& L) {
   uint64_t marks = 1ull;
 #pragma unroll 1
@@ -272,9 +309,12 @@ XE_DEV void obj_gc(XeLane& L) {
   marks |= 1ull;
   L.oused = marks;
 }
+#endif
 
 XE_DEV int obj_alloc(XeLane& L) {
+#if !defined(XE_MEM_FIELDS)
   if (L.oused == ~0ull) obj_gc(L);
+#endif
   if (L.oused == ~0ull) return -1;
   int id = __builtin_ctzll(~L.oused);
   L.oused |= 1ull << id;
@@ -310,6 +350,19 @@ XE_DEV int reg_inplace(XeLane& L, int d, int64_t v) {
 }
 
 // ------------------------------------------------------------------ footprints
+// descriptor of map m from the LDS table (only the fields a caller uses survive optimisation)
+XE_DEV XeDevMap map_desc(const XeLane& L, uint32_t m) {
+  XeDevMap M;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&M);
+  XE_LP(const uint32_t) src = (XE_LP(const uint32_t))(L.maps + m);
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(XeDevMap) / 4; k++) d[k] = src[k];
+#if defined(XE_JIT_GEOM)
+  xe_jit_geom(m, M);  // per-program kernel: map geometry as compile-time constants
+#endif
+  return M;
+}
+
 XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
   uint64_t vs = M.value_size;
   if (vs == 0) return ~0ull;
@@ -349,7 +402,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   // map memories only (packet accesses take the header-window path)
   uint32_t c = xe_h_cls(h);
   uint32_t m = xe_h_map(h);
-  const XeDevMap& M = P.maps[m];
+  const XeDevMap M = map_desc(L, m);
   B.map = m;
   if (!XE_HAS_HASH || (XE_HAS_ARRAY && c == XE_H_ARRAY)) {
     B.base = M.vals; B.len = int64_t(M.vals_bytes); B.array = true; return true;
@@ -400,33 +453,41 @@ XE_DEV void store_le(uint8_t* p0, int size, uint64_t x) {
   for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
 }
 
-// reads/writes of the LDS header copy (4-byte aligned base per lane)
-XE_DEV uint64_t hdr_read(const uint8_t* p, int size) {
-  const uintptr_t a = uintptr_t(p);
-  if (size == 1) return *p;
-  if (size == 2 && (a & 1) == 0) return *reinterpret_cast<const uint16_t*>(p);
-  if ((a & 3) == 0) {
-    if (size == 4) return *reinterpret_cast<const uint32_t*>(p);
-    if (size == 8) return uint64_t(reinterpret_cast<const uint32_t*>(p)[0]) | (uint64_t(reinterpret_cast<const uint32_t*>(p)[1]) << 32);
-  }
-  uint64_t x = 0;
-#pragma unroll 1
-  for (int b = 0; b < size; b++) x |= uint64_t(p[b]) << (8 * b);
-  return x;
+// ---- header window (LDS): physical byte pb of this lane
+XE_DEV XE_LP(uint8_t) hdr_at(const XeLane& L, int pb) { return L.hdr + (pb >> 4) * XE_HDR_ROW + (pb & 15); }
+XE_DEV uint32_t hdr_dword(const XeLane& L, int pd) { return *(XE_LP(const uint32_t))hdr_at(L, pd); }
+
+// little-endian read of `size` bytes at logical offset off (off + size <= hdr_len): the aligned
+// dwords covering the bytes and a funnel shift, no per-byte loop and no alignment branch
+XE_DEV uint64_t hdr_read(const XeLane& L, int off, int size) {
+  const int pb = off + L.hsh;
+  if (size == 1) return *hdr_at(L, pb);
+  const int p0 = pb & ~3;
+  const int sh = (pb & 3) * 8;
+  const int last = pb + size - 1;
+  const uint64_t d0 = hdr_dword(L, p0);
+  const uint64_t d1 = hdr_dword(L, last >= p0 + 4 ? p0 + 4 : p0);
+  const uint64_t lo = (d0 | (d1 << 32)) >> sh;
+  if (size == 2) return lo & 0xffffull;
+  if (size == 4) return lo & 0xffffffffull;
+  const uint64_t d2 = hdr_dword(L, last >= p0 + 8 ? p0 + 8 : p0);
+  return sh ? (lo | (d2 << (64 - sh))) : lo;
 }
-XE_DEV void hdr_write(uint8_t* p, int size, uint64_t x) {
+XE_DEV void hdr_write(XeLane& L, int off, int size, uint64_t x) {
 #pragma unroll 1
-  for (int b = 0; b < size; b++) p[b] = uint8_t(x >> (8 * b));
+  for (int b = 0; b < size; b++) *hdr_at(L, off + L.hsh + b) = uint8_t(x >> (8 * b));
 }
 
 // packet ByteMemory access through the header window when possible
 XE_DEV uint64_t pkt_load(const XeLane& L, int64_t off, int size) {
-  if (off + size <= L.hdr_len) return hdr_read(L.hdr + off, size);
-  return load_le(L.pkt + off, size);
+  if (off + size <= L.hdr_len) return hdr_read(L, int(off), size);
+  uint64_t x = load_le(L.pkt + off, size);
+  xe_pin(x);  // wait here, on the rare path, not at the join (where it would drain the prefetch)
+  return x;
 }
 XE_DEV void pkt_store(XeLane& L, int64_t off, int size, uint64_t x) {
   store_le(L.pkt + off, size, x);
-  if (off + size <= L.hdr_len) hdr_write(L.hdr + off, size, x);
+  if (off + size <= L.hdr_len) hdr_write(L, int(off), size, x);
 }
 
 // Atomic little-endian add of `add` into the `size`-byte field at p (any alignment), truncating
@@ -590,7 +651,7 @@ XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id
   vmem_region(h, wb, len);
   if (int e = bounds(off, size, len)) return e;
   int first = vmem_byte(L, wb, off);
-#pragma unroll 1
+  XE_UNROLL_VM
   for (int i = 1; i < size; i++)
     if (vmem_byte(L, wb, off + i) != first) return XE_E_NONCONTIG;
   if (!first) return XE_E_UNINIT;
@@ -601,7 +662,7 @@ XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id
 XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
   int64_t end = off + size;
   int w0 = int(off >> 3), w1 = int((end - 1) >> 3);
-#pragma unroll 1
+  XE_UNROLL_VM
   for (int w = w0; w <= w1; w++) {
     int64_t lo = off > int64_t(w) * 8 ? off - int64_t(w) * 8 : 0;
     int64_t hi = end < int64_t(w + 1) * 8 ? end - int64_t(w) * 8 : 8;
@@ -637,7 +698,7 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (track) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, size));
+  if (track) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, size));
   val = int64_t(load_le(B.base + off, size));
   kind = XE_KIND_IMM;
   oh = 0;
@@ -686,12 +747,12 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
     vmem_region(h, wb, len);
     if (off < 0 || xe_wadd(off, count) > len) return XE_E_OOB;
     if (off >= len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
-#pragma unroll 1
+    XE_UNROLL_VM
     for (int64_t i = 0; i < count;) {
       int v = vmem_byte(L, wb, off + i);
       if (!v) { emit(i, 0); i++; continue; }
       int size = 1;
-#pragma unroll 1
+      XE_UNROLL_VM
       for (int64_t j = i + 1; j < i + 8 && j < count; j++) {
         if (vmem_byte(L, wb, off + j) != v) break;
         size++;
@@ -700,7 +761,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
       if (i + w > count) return XE_EV_PANIC | XE_P_INDEX;
       int64_t ov; uint32_t oh, ot;
       obj_get(L, v, ov, oh, ot);
-#pragma unroll 1
+      XE_UNROLL_VM
       for (int b = 0; b < w; b++) emit(i + b, uint8_t(uint64_t(ov) >> (8 * b)));
       i += w;
     }
@@ -715,7 +776,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
-  if (count > 0) fp_record(L, P, B.map, false, fp_bits(P.maps[B.map], B.array, off, int(count)));
+  if (count > 0) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, int(count)));
 #pragma unroll 1
   for (int64_t i = 0; i < count; i++) emit(i, ((XE_GP(const uint8_t))B.base)[off + i]);
   return 0;
@@ -803,7 +864,7 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
   uint32_t m;
   if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
-  const XeDevMap& M = P.maps[m];
+  const XeDevMap M = map_desc(L, m);
   const XeReg R2 = reg_get(L, 2);
   if (XE_T_KIND(R2.t) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
   if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
@@ -835,7 +896,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
   uint32_t m;
   if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
-  const XeDevMap& M = P.maps[m];
+  const XeDevMap M = map_desc(L, m);
   if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
     const XeReg R2 = reg_get(L, 2), R3 = reg_get(L, 3);
     if (XE_T_KIND(R3.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
@@ -1046,7 +1107,7 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u) {
     uint32_t m = uint32_t(u.imm);
     if (uint64_t(m) >= uint64_t(P.nmaps) + 1) return XE_E_NO_MAP;
     if (m == 0) return XE_EV_PANIC | XE_P_NIL_MAP;
-    const XeDevMap& M = P.maps[m];
+    const XeDevMap M = map_desc(L, m);
     if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {
       if (M.vals_bytes == 0) return XE_E_MAP_NOT_PTR;
       reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), int64_t(u.x), 0);
@@ -1113,7 +1174,7 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
-  fp_record(L, P, B.map, true, fp_bits(P.maps[B.map], B.array, off, size));
+  fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
   wave_atomic_add_field(L.pend, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
   return 0;
 }
@@ -1163,41 +1224,160 @@ XE_DEV int wave_min(int v) {
   return cur;
 }
 
-// Reset (emulator/vm.go:211-246) + the per-packet harness ctx for packet `i`.
-XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+// Descriptor of packet i (xsk.go:695-701 layout) as two raw words {addr}, {len | options << 32}
+// (no use of the loaded values here, so the load stays in flight until desc_fix).
+XE_DEV void desc_load(const XeParams& P, uint32_t i, bool valid, uint64_t& lo, uint64_t& hi) {
+  lo = 0;
+  hi = 0;
+  if (valid) {
+    XE_GP(const uint64_t) d = (XE_GP(const uint64_t))(P.desc + i);
+    lo = d[0];
+    hi = d[1];
+  }
+}
+// A frame outside the UMEM gets length 0, so every access to it fails the ByteMemory bounds check.
+XE_DEV void desc_fix(const XeParams& P, uint64_t lo, uint64_t hi, uint64_t& a, uint32_t& l) {
+  a = lo;
+  l = uint32_t(hi);
+  if (a > P.umem_len || uint64_t(l) > P.umem_len - a) l = 0;
+}
+XE_DEV void desc_fetch(const XeParams& P, uint32_t i, bool valid, uint64_t& a, uint32_t& l) {
+  uint64_t lo, hi;
+  desc_load(P, i, valid, lo, hi);
+  desc_fix(P, lo, hi, a, l);
+}
+
+#if defined(__HIPCC__)
+// One LDS-DMA row: 16 bytes per lane from src into LDS at d + lane * 16 (d wave-uniform). Inline asm
+// on purpose: the compiler would otherwise make every later LDS read of the kernel wait for the DMA
+// (vmcnt(0)), which serialises the prefetch with the work it is meant to overlap. The matching wait
+// is explicit (hdr_wait).
+XE_DEV void glds16(XE_GP(const uint8_t) src, uint32_t d) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(d) : "memory");
+}
+#endif
+
+// Issue the LDS-DMA of a packet's header window into buffer `buf` (wave-uniform). Returns false
+// (nothing issued for this lane) when the rows would run past the UMEM; lane_stage then copies the
+// bytes one by one. Rows beyond the fourth are fetched only when some lane of the wave is misaligned.
+XE_DEV bool hdr_issue(const XeParams& P, XE_LP(uint8_t) buf, uint64_t a, bool valid) {
+  const uint64_t al = a & ~uint64_t(15);
+  const bool need5 = (a & 15) != 0;
+  const bool fast = valid && al + (need5 ? 80u : 64u) <= P.umem_len;
+  const bool any5 = xe_ballot(fast && need5) != 0;
+  if (fast) {
+#if defined(__HIPCC__)
+    XE_GP(const uint8_t) src = (XE_GP(const uint8_t))(P.umem + al);
+    const uint32_t d = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(buf)))));
+    glds16(src, d);
+    glds16(src + 16, d + XE_HDR_ROW);
+    glds16(src + 32, d + 2 * XE_HDR_ROW);
+    glds16(src + 48, d + 3 * XE_HDR_ROW);
+    if (any5) glds16(src + 64, d + 4 * XE_HDR_ROW);
+#else
+    for (int k = 0; k < (any5 ? 5 : 4); k++)
+      for (int b = 0; b < 16; b++) buf[k * XE_HDR_ROW + b] = P.umem[al + 16 * k + b];
+#endif
+  }
+  return fast;
+}
+
+// the LDS-DMA writes of this wave have landed (the compiler does not track them for LDS reads)
+XE_DEV void hdr_wait() {
+#if defined(__HIPCC__)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
+
+// Reset (emulator/vm.go:211-246) + the per-packet harness ctx for the packet
+// whose descriptor (a, l) was fetched by desc_fetch and whose window was issued into buffer `buf`
+// (hdr_issue returned `fast`; hdr_wait done).
+XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uint32_t l, bool fast,
+                       XE_LP(uint8_t) buf) {
 #pragma unroll
   for (int r = 0; r < 10; r++) reg_replace(L, r, XE_KIND_IMM, 0, 0, 0);
   reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
   reg_replace(L, 1, XE_KIND_MEMPTR, xe_h_make(XE_H_CTX, 0, 0), 0, 0);
   L.dirty = 0;
-  L.oused = 0x7full;
+  L.oused = 0x7full | (XE_OBJ_LIMIT >= 64 ? 0ull : (~0ull << (XE_OBJ_LIMIT & 63)));
   L.odef = 0x7eull;
   L.pkt = P.umem;
   L.plen = 0;
   L.hdr_len = 0;
+  L.hdr = buf + xe_lane() * 16;
+  L.hsh = fast ? int(a & 15) : 0;
   if (valid) {
-    xe_desc dsc = P.desc[i];
-    uint64_t a = dsc.addr, l = dsc.len;
-    if (a > P.umem_len || l > P.umem_len - a) l = 0;
     L.pkt = P.umem + a;
     L.plen = int64_t(l);
-    // stage the header window: 16 independent dword loads when aligned and inside the buffer
     const int hl = l < XE_HDR_WIN ? int(l) : XE_HDR_WIN;
     L.hdr_len = hl;
-    if ((a & 3) == 0 && a + XE_HDR_WIN <= P.umem_len) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(L.pkt);
-      uint32_t w[XE_HDR_WIN / 4];
-#pragma unroll
-      for (int k = 0; k < XE_HDR_WIN / 4; k++) w[k] = src[k];
-#pragma unroll
-      for (int k = 0; k < XE_HDR_WIN / 4; k++) reinterpret_cast<uint32_t*>(L.hdr)[k] = w[k];
-    } else {
+    if (!fast) {
 #pragma unroll 1
-      for (int b = 0; b < hl; b++) L.hdr[b] = L.pkt[b];
+      for (int b = 0; b < hl; b++) *hdr_at(L, b) = ((XE_GP(const uint8_t))L.pkt)[b];
     }
   }
   L.ingress = P.ingress;
   L.rxq = P.rxq;
+}
+
+// synchronous form (ordered mode): descriptor, window, wait, stage into buffer 0
+XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+  uint64_t a;
+  uint32_t l;
+  desc_fetch(P, i, valid, a, l);
+  const bool fast = hdr_issue(P, L.hdrbuf, a, valid);
+  hdr_wait();
+  lane_stage(L, P, valid, a, l, fast, L.hdrbuf);
+}
+
+// Parallel-mode driver: wave `wave` of `nwaves` walks chunks wave, wave + nwaves, ... of XE_WAVE
+// packets (one per lane). Software-pipelined: while chunk c executes, the header window of the next
+// chunk and the descriptor of the one after are already in flight, so HBM latency overlaps the
+// interpretation instead of stalling every chunk twice (descriptor -> header). The abort flag (an
+// ordered write somewhere in the batch) is polled the same way, one chunk behind.
+// body(i, valid) runs the staged packet and calls lane_finish; all lanes call it together.
+template <class Body>
+XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32_t nwaves, Body body) {
+  const uint32_t lane = uint32_t(xe_lane());
+  const uint32_t nchunks = (P.n + (XE_WAVE - 1)) / XE_WAVE;
+  uint32_t c = wave;
+  if (c >= nchunks) return;
+  uint32_t i0 = c * XE_WAVE + lane;
+  bool v0 = i0 < P.n;
+  uint64_t a0;
+  uint32_t l0;
+  desc_fetch(P, i0, v0, a0, l0);
+  uint32_t c1 = c + nwaves;
+  uint32_t i1 = c1 * XE_WAVE + lane;
+  bool v1 = c1 < nchunks && i1 < P.n;
+  uint64_t r1lo, r1hi;  // raw descriptor of chunk c1, in flight
+  desc_load(P, i1, v1, r1lo, r1hi);
+  uint32_t cur = 0;  // buffer of chunk c (wave-uniform)
+  bool f0 = hdr_issue(P, L.hdrbuf, a0, v0);
+  for (;;) {
+    hdr_wait();  // window of chunk c and descriptor of chunk c1 (issued a whole chunk ago)
+    lane_stage(L, P, v0, a0, l0, f0, L.hdrbuf + cur * XE_HDR_BUF);
+    // in flight during body(c): the window of chunk c1, the descriptor of chunk c2, the abort flag
+    uint64_t a1;
+    uint32_t l1;
+    desc_fix(P, r1lo, r1hi, a1, l1);
+    const bool f1 = hdr_issue(P, L.hdrbuf + (cur ^ 1u) * XE_HDR_BUF, a1, v1);
+    const uint32_t c2 = c1 + nwaves;
+    const uint32_t i2 = c2 * XE_WAVE + lane;
+    const bool v2 = c2 < nchunks && i2 < P.n;
+    desc_load(P, i2, v2, r1lo, r1hi);
+    const uint32_t abort_flags = xe_load_relaxed32(P.flags);
+    body(i0, v0);
+    if (c1 >= nchunks) break;
+    // a lane elsewhere needed an ordered write: this run will be discarded, stop early
+    if (xe_readfirst(int(abort_flags)) & XE_FLAG_ORDERED) break;
+    i0 = i1; v0 = v1; a0 = a1; l0 = l1; f0 = f1;
+    c1 = c2; i1 = i2; v1 = v2;
+    cur ^= 1u;
+  }
+  hdr_wait();  // no LDS-DMA may be outstanding when the wave retires
 }
 
 // map an exec_uop error to the lane's final status/code
@@ -1253,6 +1433,22 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
 }
 
+// Copy the map descriptor table into LDS (all threads of the block; barrier inside): helpers read
+// map fields with LDS loads (lgkmcnt only) instead of vector global loads whose vmcnt wait would
+// also drain the header prefetch.
+XE_DEV void stage_maps(XeLane& L, const XeParams& P, XE_LP(XeDevMap) lds) {
+#if defined(__HIPCC__)
+  const uint32_t words = (P.nmaps + 1) * uint32_t(sizeof(XeDevMap) / 4);
+  for (uint32_t t = threadIdx.x; t < words; t += blockDim.x)
+    ((XE_LP(uint32_t))lds)[t] = ((XE_GP(const uint32_t))P.maps)[t];
+  __syncthreads();
+  L.maps = lds;
+#else
+  (void)lds;
+  L.maps = P.maps;
+#endif
+}
+
 XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
   L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
   L.pend = pend;
@@ -1268,10 +1464,9 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   for (int st = 0; st < 8; st++) L.acc_status[st] = 0;
 }
 
-// Interpreter engine: runs the harness for packet `i` on this lane (valid=false: the lane idles).
-// All lanes of the wave must call this together.
-XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
-  lane_reset(L, P, i, valid);
+// Interpreter engine: runs the harness for the staged packet `i` on this lane (valid=false: the lane
+// idles). All lanes of the wave must call this together.
+XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   int status = valid ? -1 : XE_ST_OK;  // -1 = running
   int code = 0;
   int32_t pc = 0, res_pc = 0;
@@ -1305,6 +1500,11 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
     }
   }
   lane_finish(L, P, i, valid, status, code, res_pc, steps);
+}
+
+XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+  lane_reset(L, P, i, valid);
+  run_staged(L, P, i, valid);
 }
 
 // flush per-lane footprints of maps 1..4 (wave OR-reduction) and the batch statistics: one atomic

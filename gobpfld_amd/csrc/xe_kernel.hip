@@ -1,19 +1,21 @@
 // xe_kernel.hip — gfx950 kernels of the batched eBPF/XDP emulator.
 //
 // xe_interp_kernel: one lane per packet (wave64), grid-stride over 64-packet chunks in parallel
-// mode; a single lane walking the packets in order in sequential mode (exact fallback for
+// mode (software-pipelined, parallel_packets); a single lane walking the packets in order in sequential mode (exact fallback for
 // order-dependent map effects). xe_delta_kernel / xe_apply_delta_kernel: u64 counter deltas for
 // the multi-GPU all-reduce.
 #include "xe_interp.h"
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[256 * XE_HDR_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[4 * XE_HDR_WAVE_BYTES];
   __shared__ XePend pend_lds[4];
+  extern __shared__ __attribute__((aligned(16))) uint8_t xe_dyn_lds[];  // (nmaps + 1) map descriptors
   XeMem M;
   XeLane L;
   L.mem = &M;
-  L.hdr = hdr_lds + threadIdx.x * XE_HDR_STRIDE;
+  L.hdrbuf = (XE_LP(uint8_t))(hdr_lds + (threadIdx.x >> 6) * XE_HDR_WAVE_BYTES);
   const int lane = xe_lane();
+  stage_maps(L, P, (XE_LP(XeDevMap))xe_dyn_lds);
   wave_state_init(L, P, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, &pend_lds[threadIdx.x >> 6]);
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
@@ -21,13 +23,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   } else {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t nchunks = (P.n + 63u) >> 6;
-    for (uint32_t c = wave; c < nchunks; c += nwaves) {
-      // a lane elsewhere needed an ordered write: this run will be discarded, stop early
-      if (__builtin_amdgcn_readfirstlane(xe_load_relaxed32(P.flags)) & XE_FLAG_ORDERED) break;
-      const uint32_t i = c * 64u + uint32_t(lane);
-      run_packet(L, P, i, i < P.n);
-    }
+    parallel_packets(L, P, wave, nwaves, [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });
   }
   flush_wave_state(L, P);
 }
@@ -46,8 +42,14 @@ extern "C" __global__ void xe_apply_delta_kernel(unsigned long long* cur, const 
 
 // host-side launchers (called from xe_runtime.cpp)
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
-  hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), 0, s, *P);
+  hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// resident 256-thread blocks per CU for the interpreter kernel (grid sizing)
+extern "C" int xe_interp_occupancy(uint32_t nmaps) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, xe_interp_kernel, 256, (nmaps + 1) * sizeof(XeDevMap)) != hipSuccess) return 0;
+  return nb;
 }
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s) {
   uint32_t blocks = uint32_t(nwords / 256 + 1);

@@ -28,8 +28,11 @@ typedef hipStream_t xe_stream_t;
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
-extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, unsigned mapkinds, bool* cyclic, const char** err);
+extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
+                            const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
+extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
+extern "C" int xe_interp_occupancy(uint32_t nmaps);
 #endif
 
 namespace {
@@ -47,13 +50,15 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeMem M;
   XeLane L;
   L.mem = &M;
-  uint8_t hdrbuf[XE_HDR_STRIDE];
-  L.hdr = hdrbuf;
+  static uint8_t hdrbuf[XE_HDR_WAVE_BYTES];
+  L.hdrbuf = hdrbuf;
   XePend pend;
+  stage_maps(L, *P, nullptr);
   wave_state_init(L, *P, 0, &pend);
-  for (uint32_t i = 0; i < P->n; i++) {
-    if (P->mode == XE_MODE_PARALLEL && (*P->flags & XE_FLAG_ORDERED)) break;
-    run_packet(L, *P, i, true);
+  if (P->mode == XE_MODE_PARALLEL) {
+    parallel_packets(L, *P, 0, 1, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
+  } else {
+    for (uint32_t i = 0; i < P->n; i++) run_packet(L, *P, i, true);
   }
   flush_wave_state(L, *P);
   return 0;
@@ -75,6 +80,8 @@ struct Timer {
   void fini() {}
 };
 int set_device(int) { return 0; }
+int blocks_per_cu(void*, uint32_t) { return 1; }
+int cu_count(int) { return 1; }
 #else
 int dev_alloc(void** p, size_t n) { return hipMalloc(p, n ? n : 8) == hipSuccess ? 0 : -1; }
 void dev_free(void* p) { if (p) (void)hipFree(p); }
@@ -95,6 +102,13 @@ struct Timer {
   static float ms(const Timer& a, const Timer& b) { float m = 0; (void)hipEventElapsedTime(&m, a.e, b.e); return m; }
 };
 int set_device(int d) { return hipSetDevice(d) == hipSuccess ? 0 : -1; }
+// resident 256-thread blocks per CU of the kernel that will run (0 = unknown)
+int blocks_per_cu(void* jit, uint32_t nmaps) { return jit ? xe_jit_occupancy(jit, nmaps) : xe_interp_occupancy(nmaps); }
+int cu_count(int dev) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return n;
+}
 #endif
 
 // ------------------------------------------------------------------ decoder + translator
@@ -324,6 +338,11 @@ struct xe_vm {
   size_t d_maps_n = 0;
   std::vector<XeDevMap> dm_uploaded;  // host copy of the device map table (upload only on change)
   unsigned long long* d_aux = nullptr;  // [0..15] stats, [16] flags, [32..] footprints
+  // grid sizing: CU count and resident blocks per CU of each kernel (-1 = not queried yet)
+  int cus = -1, occ_interp = -1, occ_jit = -1;
+  void* occ_jit_fn = nullptr;
+  uint32_t occ_nmaps = 0;
+  uint32_t last_grid = 0;
   // host-run staging
   void* d_umem = nullptr; size_t d_umem_cap = 0;
   void* d_usnap = nullptr; size_t d_usnap_cap = 0;  // packet bytes before a replayable parallel pass
@@ -335,6 +354,7 @@ struct xe_vm {
   uint32_t last_flags = 0;
   // per-program kernel (JIT engine) for the current entry program
   int32_t jit_idx = -1;
+  size_t jit_nmaps = 0;
   void* jit_fn = nullptr;
   bool jit_cyclic = false;
   std::string jit_error;
@@ -459,10 +479,15 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   return XE_OK;
 }
 
-uint32_t grid_blocks(uint32_t n) {
+// Parallel-mode grid: exactly the blocks that are resident at once (persistent waves walking the
+// chunks, see parallel_packets), never more than one 64-packet chunk per wave. A second generation of
+// blocks would run its full share after the first finishes, and every extra wave adds its per-wave
+// flush (map atomics, statistics) to the same few addresses.
+uint32_t grid_blocks(uint32_t n, int per_cu, int cus) {
   uint64_t chunks = (uint64_t(n) + 63) / 64;
   uint64_t blocks = (chunks + 3) / 4;  // 4 waves per 256-thread block
-  const uint64_t maxb = 256ull * 16;   // grid-stride beyond this
+  uint64_t maxb = (per_cu > 0 && cus > 0) ? uint64_t(per_cu) * uint64_t(cus) : 256ull * 4;
+  if (const char* e = getenv("XE_MAX_BLOCKS")) maxb = std::max(1ll, atoll(e));  // tuning experiments
   return uint32_t(std::max<uint64_t>(1, std::min(blocks, maxb)));
 }
 
@@ -570,7 +595,7 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
   }
   m.host_dirty = true;
   vm->maps.push_back(std::move(m));
-  vm->jit_idx = -1;  // map kinds are compiled into the per-program kernel
+  vm->jit_idx = -1;  // map geometry is compiled into the per-program kernel
   if (idx) *idx = int32_t(vm->maps.size() - 1);
   return XE_OK;
 }
@@ -794,14 +819,15 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   void* jit = nullptr;
 #ifndef XE_HOSTSIM
   if (engine != XE_ENGINE_INTERP) {
-    if (vm->jit_idx != vm->entry) {
+    if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size()) {
+      // the kernel is specialised on the program and the map geometry (xe_jit.cpp)
       const auto& prog = vm->programs[vm->entry];
       const char* jerr = "";
-      unsigned kinds = 0;
-      for (size_t i = 1; i < vm->maps.size(); i++) kinds |= vm->maps[i].dkind == XE_DM_ARRAY ? 1u : vm->maps[i].dkind == XE_DM_HASH ? 2u : 0u;
-      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, kinds, &vm->jit_cyclic, &jerr);
+      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
+                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &jerr);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
+      vm->jit_nmaps = vm->maps.size();
     }
     jit = vm->jit_fn;
     // acyclic kernels carry no budget checks: exact only while the budget cannot be reached
@@ -831,7 +857,16 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   } else {
     P.mode = XE_MODE_PARALLEL;
-    if (launch(&P, grid_blocks(n), 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    if (vm->cus < 0) vm->cus = cu_count(vm->settings.device);
+    int& occ = jit ? vm->occ_jit : vm->occ_interp;
+    if ((jit && jit != vm->occ_jit_fn) || P.nmaps != vm->occ_nmaps) {
+      vm->occ_jit_fn = jit ? jit : vm->occ_jit_fn;
+      vm->occ_nmaps = P.nmaps;
+      vm->occ_jit = vm->occ_interp = -1;
+    }
+    if (occ < 0) occ = blocks_per_cu(jit, P.nmaps);
+    vm->last_grid = grid_blocks(n, occ, vm->cus);
+    if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   }
   vm->t1.rec(s);
   std::vector<unsigned long long> aux(aux_used);
@@ -885,6 +920,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     stats->kernel_ms = kms;
     stats->total_ms = kms;
     stats->engine_used = jit ? XE_ENGINE_JIT : XE_ENGINE_INTERP;
+    stats->grid_blocks = used == XE_MODE_PARALLEL ? vm->last_grid : 1;
   }
   return XE_OK;
 }

@@ -62,7 +62,7 @@ class BatchResult:
 def _stats_dict(s: N.BatchStats) -> dict:
     return {"packets": s.packets, "steps": s.steps, "status_count": list(s.status_count),
             "mode_used": s.mode_used, "conflict": s.conflict, "kernel_ms": s.kernel_ms,
-            "total_ms": s.total_ms, "engine_used": s.engine_used}
+            "total_ms": s.total_ms, "engine_used": s.engine_used, "grid_blocks": s.grid_blocks}
 
 
 class VM:

@@ -175,7 +175,7 @@ typedef struct xe_batch_stats {
     float kernel_ms;           /* device time of the interpreter launch(es) */
     float total_ms;            /* device time of the whole call */
     uint32_t engine_used;      /* XE_ENGINE_INTERP or XE_ENGINE_JIT */
-    uint32_t reserved;
+    uint32_t grid_blocks;      /* blocks of the parallel launch (1 for the ordered path) */
 } xe_batch_stats;
 
 typedef struct xe_vm xe_vm;

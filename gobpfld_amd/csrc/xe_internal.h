@@ -98,6 +98,12 @@ struct XeDevMap {
   uint32_t* count;      // HASH: number of entries (device word)
   uint32_t cap;         // HASH: power-of-two slot count
   uint32_t kwords;      // HASH: (key_size+7)/8
+  // replicas of the value region for deferred 8-byte adds in parallel mode (wave w adds into replica
+  // w % nrep; the runtime folds them into vals after the launch and leaves them zeroed)
+  uint8_t* rep;
+  uint64_t rep_stride;  // bytes between replicas
+  uint32_t nrep;        // 1 = adds go to vals directly
+  uint32_t pad_;
 };
 
 // Word-wise multiplicative hash over the zero-padded key words. The reference hashes with sha256
@@ -118,6 +124,10 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 
 // kernel-side status of a lane beyond the public XE_ST_*
 #define XE_ST_INTERNAL_ORDERED 6
+
+// replica record words: [0] steps, [1..8] status histogram, [9..12] atomic width classes (4 bits per
+// map: 1, 2, 4, 8 bytes), [16 + 2m] read mask and [17 + 2m] atomic mask of map m
+#define XE_REC_WIDTH0 9
 
 // flags word bits (device -> host)
 #define XE_FLAG_ORDERED 1u   // a lane needed a non-commutative map write in parallel mode

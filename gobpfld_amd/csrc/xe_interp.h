@@ -93,6 +93,12 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_HAS_HASH 1
 #endif
 
+// maps whose read / atomic footprints a lane keeps in registers (the rest OR straight into the wave's
+// record); a per-program kernel sets it to the VM's map count
+#ifndef XE_FP_MAPS
+#define XE_FP_MAPS 4
+#endif
+
 // Packet header window staged in LDS per lane (the first 64 bytes are the hot bytes).
 // The window is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR destination) from the 16-byte
 // aligned address below the packet start, as XE_HDR_ROWS rows of 16 bytes per lane; one DMA
@@ -100,7 +106,7 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 // l * 16). A lane's logical byte b lives at physical byte b + hsh (hsh = addr & 15) of its rows.
 // Two such buffers per wave: the next chunk's window is in flight while the current one executes.
 #define XE_HDR_WIN 64
-#define XE_HDR_ROWS 5                              // 64 bytes + up to 15 bytes of misalignment
+#define XE_HDR_ROWS 4                              // 64 bytes from the aligned-down packet address
 #define XE_HDR_ROW (XE_WAVE * 16)                  // bytes of one row for the whole wave
 #define XE_HDR_BUF (XE_HDR_ROWS * XE_HDR_ROW)      // one buffer
 #define XE_HDR_WAVE_BYTES (2 * XE_HDR_BUF)         // double buffer per wave
@@ -161,15 +167,21 @@ XE_DEV void xm_set_bm(XeMem& M, int w, uint64_t v) { M.bm[w] = v; }
 #define XE_UNROLL_VM _Pragma("unroll")
 #endif
 
-// per-wave combining cache of deferred map atomics (parallel mode only), kept in LDS and touched by
-// one lane at a time (the aggregation leader)
-#define XE_PEND 8
-struct XePend {
-  unsigned long long addr[XE_PEND];
-  unsigned long long sum[XE_PEND];
-  int size[XE_PEND];
-  int next;  // round-robin victim
+// Per-wave accumulator table of deferred map adds (parallel mode only), in LDS: XE_ACC direct-mapped
+// entries {tag = field address | size << 56, sum, score}. A field that owns its entry is added with
+// an LDS atomic; every other add goes straight to HBM as one vector atomic. An entry is claimed when
+// free, and taken over (its sum flushed to HBM) when misses have worn its score down, so the hot
+// counters of a skewed stream end up owning entries and reach HBM once per wave instead of once per
+// packet (C3's Zipf flows, C2's per-proto array). Flushed when the wave retires (flush_wave_state).
+#ifndef XE_ACC
+#define XE_ACC 64
+#endif
+struct XeAcc {
+  unsigned long long tag[XE_ACC];
+  unsigned long long sum[XE_ACC];
+  int score[XE_ACC];
 };
+typedef XeAcc XePend;
 
 struct XeReg {
   int64_t v;   // RegisterValue.Value()
@@ -210,14 +222,16 @@ struct XeLane {
   int32_t hdr_len;         // min(plen, 64): bytes served from the window
   int32_t hsh;             // physical offset of logical byte 0 in the lane's rows
   // per-lane map footprints for maps 1..4 (others go straight to global)
-  uint64_t fpr[4];
-  uint64_t fpa[4];
+  uint64_t fpr[XE_FP_MAPS];
+  uint64_t fpa[XE_FP_MAPS];
   // xdp_md ingress_ifindex / rx_queue_index values of the lazily materialised ctx objects 4, 5
   uint32_t ingress, rxq;
   // wave-uniform batch statistics, flushed once per wave (flush_wave_state)
   uint64_t acc_steps;
   uint32_t acc_status[8];
   unsigned long long* rep;  // this wave's statistics / footprint replica record
+  uint32_t wave;            // global wave index (map value replica = wave % nrep)
+  uint32_t awidth;          // atomic width classes used on maps 1..4 (4 bits per map)
   XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
 };
 
@@ -377,10 +391,18 @@ XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
   return top & ~((1ull << lo) - 1ull);
 }
 
+// atomic adds of different widths on one map do not commute in general (a narrow add stops its
+// carry at its own top byte): the host treats a map with more than one width class as a conflict
+XE_DEV void width_record(XeLane& L, uint32_t m, int size) {
+  const uint32_t cls = size == 8 ? 3u : size == 4 ? 2u : size == 2 ? 1u : 0u;
+  if (m >= 1 && m <= 4) L.awidth |= 1u << (4 * m + cls);
+  else xe_atomic_or64(&L.rep[XE_REC_WIDTH0 + m / 16], 1ull << (4 * (m % 16) + cls));
+}
+
 XE_DEV void fp_record(XeLane& L, const XeParams& P, uint32_t m, bool atomic, uint64_t bits) {
-  if (m >= 1 && m <= 4) {
+  if (m >= 1 && m <= XE_FP_MAPS) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < XE_FP_MAPS; k++) {
       if (uint32_t(k + 1) == m) {
         if (atomic) L.fpa[k] |= bits; else L.fpr[k] |= bits;
       }
@@ -526,111 +548,104 @@ XE_DEV void atomic_add_field(uint8_t* p, int size, uint64_t add) {
   }
 }
 
-// Map atomics from the lanes active at this instruction, aggregated per distinct (address, size):
-// one leader lane adds the sum of its peers' addends (exact: the field add is modulo 2^(8*size), so
-// the sum of several adds equals one add of their sum). Removes same-address contention for hot
-// counters (C2's per-proto array, hot flows).
-// XE_PEND_MODE: 0 = apply immediately, 1 = fully associative branch-free probe, 2 = early-exit probe
-#ifndef XE_PEND_MODE
-#define XE_PEND_MODE 1
-#endif
-#ifndef XE_SINGLE_BYPASS
-#define XE_SINGLE_BYPASS 1
-#endif
-#ifndef XE_UNIFORM_SUM
-#define XE_UNIFORM_SUM 1
-#endif
-
-// pd is never selected against null (that would turn the LDS pointer generic: flat instructions)
-XE_DEV void pend_add(XePend* pd, uint64_t addr, int size, uint64_t sum) {
-  if (XE_PEND_MODE == 0) { atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(addr)), size, sum); return; }
-  int hit = -1, fr = -1;
-  if (XE_PEND_MODE == 2) {
-#pragma unroll
-    for (int k = 0; k < XE_PEND; k++) {
-      const int ts = pd->size[k];
-      if (ts == size && pd->addr[k] == addr) { hit = k; break; }
-      if (ts == 0) { fr = k; break; }
-    }
-  } else {
-    // all tags are loaded at once; the hit / free entry is selected in registers
-    uint64_t ta[XE_PEND];
-    int ts[XE_PEND];
-#pragma unroll
-    for (int k = 0; k < XE_PEND; k++) { ta[k] = pd->addr[k]; ts[k] = pd->size[k]; }
-#pragma unroll
-    for (int k = XE_PEND - 1; k >= 0; k--) {
-      hit = (ts[k] == size && ta[k] == addr) ? k : hit;
-      fr = ts[k] == 0 ? k : fr;
-    }
-  }
-  if (hit >= 0) { pd->sum[hit] += sum; return; }
-  int k = fr;
-  if (k < 0) {  // full: evict (apply) a round-robin victim
-    k = pd->next;
-    pd->next = (k + 1) & (XE_PEND - 1);
-    atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
-  }
-  pd->addr[k] = addr; pd->size[k] = size; pd->sum[k] = sum;
-}
-
-XE_DEV void pend_flush(XePend* pd) {
-#pragma unroll
-  for (int k = 0; k < XE_PEND; k++) {
-    if (pd->size[k]) atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(pd->addr[k])), pd->size[k], pd->sum[k]);
-    pd->size[k] = 0;
-  }
-}
-
-XE_DEV void wave_atomic_add_field(XePend* pend, bool defer, uint8_t* p, int size, uint64_t add) {
 #if defined(__HIPCC__)
-  const uint64_t addr = uint64_t(uintptr_t(p));
-  unsigned long long remaining = xe_ballot(true);
-  const int me = xe_lane();
-  // parallel pre-probe: every active lane looks its field up in the wave's cache at once (broadcast
-  // LDS reads), so a group of one whose counter is already cached (e.g. the hot counter reached from
-  // a rare parse path) still accumulates locally, while unique addresses skip the LDS entirely
-  int hk = -1;
-  if (defer) {
-#pragma unroll
-    for (int k = XE_PEND - 1; k >= 0; k--) hk = (pend->size[k] == size && pend->addr[k] == addr) ? k : hk;
+XE_DEV unsigned long long xe_lds_cas64(XE_LP(unsigned long long) p, unsigned long long c, unsigned long long v) {
+  __hip_atomic_compare_exchange_strong(p, &c, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  return c;
+}
+XE_DEV void xe_lds_add64(XE_LP(unsigned long long) p, unsigned long long v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+XE_DEV unsigned long long xe_lds_xchg64(XE_LP(unsigned long long) p, unsigned long long v) {
+  return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+XE_DEV int xe_lds_add32(XE_LP(int) p, int v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+#else
+XE_DEV unsigned long long xe_lds_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
+  unsigned long long o = *p;
+  if (o == c) *p = v;
+  return o;
+}
+XE_DEV void xe_lds_add64(unsigned long long* p, unsigned long long v) { *p += v; }
+XE_DEV unsigned long long xe_lds_xchg64(unsigned long long* p, unsigned long long v) { unsigned long long o = *p; *p = v; return o; }
+XE_DEV int xe_lds_add32(int* p, int v) { int o = *p; *p += v; return o; }
+#endif
+
+XE_DEV uint32_t acc_slot(uint64_t addr) {
+  return uint32_t(((addr >> 2) * 0x9E3779B97F4A7C15ull) >> 58) & (XE_ACC - 1);
+}
+
+// One HBM add of a (deferred) sum into an aligned 4/8-byte field of map m. 8-byte adds go to this
+// wave's replica of the value region when the map has replicas, which spreads a hot counter over
+// nrep addresses (same-address atomics serialise at the memory side).
+XE_DEV void field_add(const XeLane& L, uint32_t m, uint64_t addr, int size, uint64_t v) {
+  if (size == 8) {
+    const XeDevMap M = map_desc(L, m);
+    if (M.nrep > 1) addr = uint64_t(uintptr_t(M.rep)) + uint64_t(L.wave % M.nrep) * M.rep_stride + (addr - uint64_t(uintptr_t(M.vals)));
+    xe_atomic_add64(reinterpret_cast<unsigned long long*>(uintptr_t(addr)), v);
+  } else {
+    xe_atomic_add32(reinterpret_cast<unsigned int*>(uintptr_t(addr)), uint32_t(v));
   }
-  while (remaining) {
-    const int leader = __builtin_ctzll(remaining);
-    const uint64_t la = (uint64_t(uint32_t(xe_readlane(int(addr >> 32), leader))) << 32) |
-                        uint64_t(uint32_t(xe_readlane(int(uint32_t(addr)), leader)));
-    const int ls = xe_readlane(size, leader);
-    const unsigned long long peers = xe_ballot(addr == la && size == ls) & remaining;
-    uint64_t sum = 0;
-    unsigned long long m = peers;
-    if (XE_UNIFORM_SUM) {  // counters: every peer adds the same amount
-      const uint64_t lv = (uint64_t(uint32_t(xe_readlane(int(add >> 32), leader))) << 32) |
-                          uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), leader)));
-      if ((xe_ballot(add == lv) & peers) == peers) {
-        sum = lv * uint64_t(__builtin_popcountll(peers));
-        m = 0;
+}
+// accumulator tag = field address (48 bits) | map << 48 | size << 56
+XE_DEV void acc_apply(const XeLane& L, unsigned long long tag, unsigned long long v) {
+  field_add(L, uint32_t((tag >> 48) & 0xffu), tag & 0xffffffffffffull, int(tag >> 56), v);
+}
+
+// Add `add` to the `size`-byte field at p of map m. Deferred (parallel mode): naturally aligned 4/8-
+// byte fields go through the wave's accumulator table, and 8-byte adds that reach HBM go to the
+// wave's replica. Exact in every case: the field add is modulo 2^(8*size), so adding a sum later
+// equals adding its parts now; an entry changes owner only after its sum has been taken (exchange)
+// and before any lane of this instruction adds to it (the adds re-read the tag after the claim /
+// take-over step), so no part is lost or credited to another field.
+XE_DEV void wave_atomic_add_field(XeLane& L, uint32_t m, bool defer, uint8_t* p, int size, uint64_t add) {
+#if defined(XE_DEBUG_NO_ATOMIC)  // cost experiments only: map adds are dropped (results are wrong)
+  return;
+#endif
+  XePend* acc = L.pend;
+  const uint64_t addr = uint64_t(uintptr_t(p));
+  if (defer && (size == 8 || size == 4) && (addr & uint64_t(size - 1)) == 0) {
+    const uint64_t tag = addr | (uint64_t(m) << 48) | (uint64_t(size) << 56);
+    const uint32_t k = acc_slot(addr);
+    XE_LP(unsigned long long) tp = (XE_LP(unsigned long long))&acc->tag[k];
+    XE_LP(int) sp = (XE_LP(int))&acc->score[k];
+    const unsigned long long t = *tp;
+    if (t == 0) {
+      if (xe_lds_cas64(tp, 0ull, tag) == 0) *sp = 1;
+    } else if (t != tag) {
+      // a miss wears the owner's score down; the lane that exhausts it takes the entry over
+      if (xe_lds_add32(sp, -1) <= 1 && xe_lds_cas64(tp, t, tag) == t) {
+        const unsigned long long old = xe_lds_xchg64((XE_LP(unsigned long long))&acc->sum[k], 0ull);
+        *sp = 2;
+        if (old) acc_apply(L, t, old);
       }
     }
-    while (m) {
-      const int l = __builtin_ctzll(m);
-      m &= m - 1;
-      sum += (uint64_t(uint32_t(xe_readlane(int(add >> 32), l))) << 32) |
-             uint64_t(uint32_t(xe_readlane(int(uint32_t(add)), l)));
+    if (*tp == tag) {
+      xe_lds_add64((XE_LP(unsigned long long))&acc->sum[k], add);
+      if (t == tag) xe_lds_add32(sp, 1);
+      return;
     }
-    // cached field: accumulate (re-checked: an insert earlier in this loop may have evicted it);
-    // an uncached group of one gains nothing from deferral: apply it directly (fire-and-forget)
-    const int lhk = xe_readlane(hk, leader);
-    if (me == leader) {
-      if (defer && lhk >= 0 && pend->addr[lhk] == la && pend->size[lhk] == ls) pend->sum[lhk] += sum;
-      else if (defer && (!XE_SINGLE_BYPASS || __builtin_popcountll(peers) > 1)) pend_add(pend, la, ls, sum);
-      else atomic_add_field(reinterpret_cast<uint8_t*>(uintptr_t(la)), ls, sum);
-    }
-    remaining &= ~peers;
+    field_add(L, m, addr, size, add);
+    return;
   }
-#else
-  if (defer) pend_add(pend, uint64_t(uintptr_t(p)), size, add);
-  else atomic_add_field(p, size, add);
-#endif
+  atomic_add_field(p, size, add);
+}
+
+// all lanes: lane k applies entry k (one vector atomic for the whole table) and clears it
+XE_DEV void acc_flush(const XeLane& L) {
+  XePend* acc = L.pend;
+#pragma unroll 1
+  for (uint32_t k0 = 0; k0 < XE_ACC; k0 += XE_WAVE) {
+    const uint32_t k = k0 + uint32_t(xe_lane());
+    const unsigned long long t = acc->tag[k];
+    if (t) {
+      if (acc->sum[k]) acc_apply(L, t, acc->sum[k]);
+      acc->tag[k] = 0;
+      acc->sum[k] = 0;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ ValueMemory access
@@ -1175,7 +1190,8 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
   fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
-  wave_atomic_add_field(L.pend, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
+  width_record(L, B.map, size);
+  wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
   return 0;
 }
 
@@ -1261,12 +1277,11 @@ XE_DEV void glds16(XE_GP(const uint8_t) src, uint32_t d) {
 
 // Issue the LDS-DMA of a packet's header window into buffer `buf` (wave-uniform). Returns false
 // (nothing issued for this lane) when the rows would run past the UMEM; lane_stage then copies the
-// bytes one by one. Rows beyond the fourth are fetched only when some lane of the wave is misaligned.
+// bytes one by one. The rows start at the 16-byte aligned address below the packet, so a misaligned
+// packet's window holds 64 - (addr & 15) of its bytes (lane_stage sets hdr_len accordingly).
 XE_DEV bool hdr_issue(const XeParams& P, XE_LP(uint8_t) buf, uint64_t a, bool valid) {
   const uint64_t al = a & ~uint64_t(15);
-  const bool need5 = (a & 15) != 0;
-  const bool fast = valid && al + (need5 ? 80u : 64u) <= P.umem_len;
-  const bool any5 = xe_ballot(fast && need5) != 0;
+  const bool fast = valid && al + XE_HDR_WIN <= P.umem_len;
   if (fast) {
 #if defined(__HIPCC__)
     XE_GP(const uint8_t) src = (XE_GP(const uint8_t))(P.umem + al);
@@ -1275,9 +1290,8 @@ XE_DEV bool hdr_issue(const XeParams& P, XE_LP(uint8_t) buf, uint64_t a, bool va
     glds16(src + 16, d + XE_HDR_ROW);
     glds16(src + 32, d + 2 * XE_HDR_ROW);
     glds16(src + 48, d + 3 * XE_HDR_ROW);
-    if (any5) glds16(src + 64, d + 4 * XE_HDR_ROW);
 #else
-    for (int k = 0; k < (any5 ? 5 : 4); k++)
+    for (int k = 0; k < XE_HDR_ROWS; k++)
       for (int b = 0; b < 16; b++) buf[k * XE_HDR_ROW + b] = P.umem[al + 16 * k + b];
 #endif
   }
@@ -1311,7 +1325,8 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   if (valid) {
     L.pkt = P.umem + a;
     L.plen = int64_t(l);
-    const int hl = l < XE_HDR_WIN ? int(l) : XE_HDR_WIN;
+    const int win = XE_HDR_WIN - L.hsh;
+    const int hl = l < uint32_t(win) ? int(l) : win;
     L.hdr_len = hl;
     if (!fast) {
 #pragma unroll 1
@@ -1451,14 +1466,13 @@ XE_DEV void stage_maps(XeLane& L, const XeParams& P, XE_LP(XeDevMap) lds) {
 
 XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
   L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
+  L.wave = wave;
+  L.awidth = 0;
   L.pend = pend;
-  if (xe_lane() == 0) {
+#pragma unroll 1
+  for (uint32_t k = uint32_t(xe_lane()); k < XE_ACC; k += XE_WAVE) { pend->tag[k] = 0; pend->sum[k] = 0; pend->score[k] = 0; }
 #pragma unroll
-    for (int k = 0; k < XE_PEND; k++) pend->size[k] = 0;
-    pend->next = 0;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
+  for (int k = 0; k < XE_FP_MAPS; k++) { L.fpr[k] = 0; L.fpa[k] = 0; }
   L.acc_steps = 0;
 #pragma unroll
   for (int st = 0; st < 8; st++) L.acc_status[st] = 0;
@@ -1510,8 +1524,13 @@ XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
 // flush per-lane footprints of maps 1..4 (wave OR-reduction) and the batch statistics: one atomic
 // per word per wave
 XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
-  if (xe_lane() == 0) pend_flush(L.pend);
+  acc_flush(L);
   unsigned long long steps = L.acc_steps;
+  unsigned int aw = L.awidth;
+#if defined(__HIPCC__)
+  for (int o = 32; o > 0; o >>= 1) aw |= __shfl_xor(aw, o);
+#endif
+  if (xe_lane() == 0 && aw) xe_atomic_or64(&L.rep[XE_REC_WIDTH0], aw);
 #if defined(__HIPCC__)
   for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o);
 #endif
@@ -1522,7 +1541,7 @@ XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
       if (L.acc_status[st]) xe_atomic_add64(&L.rep[1 + st], L.acc_status[st]);
   }
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < XE_FP_MAPS; k++) {
     unsigned long long r = L.fpr[k], a = L.fpa[k];
 #if defined(__HIPCC__)
     for (int o = 32; o > 0; o >>= 1) { r |= __shfl_xor(r, o); a |= __shfl_xor(a, o); }

@@ -40,6 +40,19 @@ extern "C" __global__ void xe_apply_delta_kernel(unsigned long long* cur, const 
     cur[i] = snap[i] + delta[i];
 }
 
+// vals += sum of the replicas; replicas := 0 (only words that received adds are written)
+extern "C" __global__ void xe_rep_fold_kernel(unsigned long long* vals, unsigned long long* rep, uint64_t stride_words,
+                                              uint32_t nrep, uint64_t nwords) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x) {
+    unsigned long long s = 0;
+    for (uint32_t k = 0; k < nrep; k++) {
+      const unsigned long long v = rep[k * stride_words + i];
+      if (v) { s += v; rep[k * stride_words + i] = 0; }
+    }
+    if (s) vals[i] += s;
+  }
+}
+
 // host-side launchers (called from xe_runtime.cpp)
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
   hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);
@@ -56,6 +69,13 @@ extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uin
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(xe_delta_kernel, dim3(blocks), dim3(256), 0, s, (const unsigned long long*)cur,
                      (const unsigned long long*)snap, (unsigned long long*)out, nwords);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s) {
+  uint32_t blocks = uint32_t(nwords / 256 + 1);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(xe_rep_fold_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)vals, (unsigned long long*)rep,
+                     stride_words, nrep, nwords);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s) {

@@ -28,6 +28,7 @@ typedef hipStream_t xe_stream_t;
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
                             const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -72,6 +73,13 @@ int launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t 
   for (uint64_t i = 0; i < nw; i++) ((uint64_t*)cur)[i] = ((const uint64_t*)snap)[i] + ((const uint64_t*)delta)[i];
   return 0;
 }
+int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t) {
+  uint64_t* v = (uint64_t*)vals;
+  uint64_t* r = (uint64_t*)rep;
+  for (uint64_t i = 0; i < nw; i++)
+    for (uint32_t k = 0; k < nrep; k++) { v[i] += r[k * sw + i]; r[k * sw + i] = 0; }
+  return 0;
+}
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
@@ -94,6 +102,7 @@ int launch_interp(const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { re
 int launch_jit(void* fn, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_jit_launch(fn, P, b, t, s); }
 int launch_delta(const void* c, const void* sn, void* o, uint64_t nw, xe_stream_t s) { return xe_launch_delta(c, sn, o, nw, s); }
 int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t nw, xe_stream_t s) { return xe_launch_apply_delta(c, sn, d, nw, s); }
+int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t s) { return xe_launch_rep_fold(v, r, sw, nrep, nw, s); }
 struct Timer {
   hipEvent_t e = nullptr;
   void init() { if (!e) (void)hipEventCreate(&e); }
@@ -272,6 +281,9 @@ struct HostMap {
   uint32_t* d_state = nullptr;
   uint32_t* d_count = nullptr;
   uint8_t* d_snap = nullptr;
+  uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
+  uint32_t nrep = 1;
+  uint64_t rep_stride = 0;
   bool host_dirty = true, dev_dirty = false;
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -382,9 +394,19 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
   return 0;
 }
 
+// Replicas of the value region for deferred 8-byte adds (XeDevMap::rep): enough to spread a hot
+// counter's atomics, bounded in memory (HBM is plentiful, but every run folds all replicas).
+uint32_t choose_nrep(uint64_t vals_alloc) {
+  if (const char* e = getenv("XE_NREP")) return uint32_t(std::max(1, atoi(e)));  // tuning experiments
+  return vals_alloc <= (8ull << 20) ? 16u : vals_alloc <= (64ull << 20) ? 8u : vals_alloc <= (256ull << 20) ? 4u : 1u;
+}
+
 int map_alloc_device(HostMap& m) {
   if (dev_alloc((void**)&m.d_vals, m.vals_alloc)) return -1;
   if (dev_alloc((void**)&m.d_snap, m.vals_alloc)) return -1;
+  m.nrep = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(m.vals_alloc) : 1u;
+  m.rep_stride = (m.vals_alloc + 255) & ~uint64_t(255);
+  if (m.nrep > 1 && dev_alloc((void**)&m.d_rep, m.rep_stride * m.nrep)) return -1;
   if (m.dkind == XE_DM_HASH) {
     if (dev_alloc((void**)&m.d_keys, std::max<size_t>(size_t(m.cap + 1) * m.kwords * 8, 8))) return -1;
     if (dev_alloc((void**)&m.d_state, size_t(m.cap + 1) * 4)) return -1;
@@ -394,8 +416,8 @@ int map_alloc_device(HostMap& m) {
 }
 
 void map_free_device(HostMap& m) {
-  dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count);
-  m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr;
+  dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count); dev_free(m.d_rep);
+  m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr; m.d_rep = nullptr;
 }
 
 int map_upload(xe_vm* vm, HostMap& m) {
@@ -463,6 +485,9 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     d.count = m.d_count;
     d.cap = m.cap;
     d.kwords = m.kwords;
+    d.rep = m.d_rep;
+    d.rep_stride = m.rep_stride;
+    d.nrep = m.nrep;
   }
   if (vm->d_maps_n < dm.size()) {
     dev_free(vm->d_maps);
@@ -592,6 +617,10 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
   if (set_device(vm->settings.device) || map_alloc_device(m)) {
     map_free_device(m);
     return fail(vm, XE_ERR_DEVICE, "device alloc (map)");
+  }
+  if (m.d_rep && (dmemset(m.d_rep, 0, m.rep_stride * m.nrep, vm->stream) || dsync(vm->stream))) {
+    map_free_device(m);
+    return fail(vm, XE_ERR_DEVICE, "replica init");
   }
   m.host_dirty = true;
   vm->maps.push_back(std::move(m));
@@ -867,6 +896,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (occ < 0) occ = blocks_per_cu(jit, P.nmaps);
     vm->last_grid = grid_blocks(n, occ, vm->cus);
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
+        return fail(vm, XE_ERR_DEVICE, "replica fold");
+    }
   }
   vm->t1.rec(s);
   std::vector<unsigned long long> aux(aux_used);
@@ -878,6 +913,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       const unsigned long long* rec = aux.data() + 16 + size_t(r) * P.rep_words;
       sum[1] += rec[0];
       for (int k = 0; k < 8; k++) sum[2 + k] += rec[1 + k];
+      for (int k = 0; k < 4; k++) sum[XE_REC_WIDTH0 + 2 + k] |= rec[XE_REC_WIDTH0 + k];
       for (uint32_t w = 0; w < 2 * (P.nmaps + 1); w++) sum[16 + w] |= rec[16 + w];
     }
   };
@@ -888,8 +924,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   if (mode != XE_MODE_SEQUENTIAL) {
     uint32_t flags = uint32_t(red[0]);
     conflict = (flags & XE_FLAG_ORDERED) != 0;
-    for (uint32_t m = 1; m <= P.nmaps && m < 64; m++)
+    for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
       if (red[16 + 2 * m] & red[16 + 2 * m + 1]) conflict = true;
+      // atomic adds of more than one width on a map do not commute (carry stops at a field's top)
+      const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
+      if (wc & (wc - 1)) conflict = true;
+    }
     if (conflict && mode == XE_MODE_AUTO) {
       // order-dependent batch: roll the maps back and replay it in packet order on one lane
       for (size_t i = 1; i < vm->maps.size(); i++) {

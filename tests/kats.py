@@ -458,6 +458,16 @@ def _(a):
     a.label("out").mov64(0, -1).exit()
 
 
+@kat("mixed_width_xadd_ordered", (OK, None),
+     maps=[(MapDef(MAP_ARRAY, 4, 8, 16), (0xFFFFFFFE).to_bytes(8, "little") + bytes(120))],
+     cite="inst_atomic.go:44-59: a 4-byte add truncates at byte 3, an 8-byte add carries: order-dependent")
+def _(a):
+    a.st(4, 10, -4, 0).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "out", imm=0)
+    a.mov64(1, 1).xadd(8, 0, 0, 1).xadd(4, 0, 0, 1).mov64(0, 2).exit()
+    a.label("out").mov64(0, -1).exit()
+
+
 @kat("xadd_then_read_conflict", (OK, None), maps=[ARRAY8], cite="atomic and read of the same bytes: order-dependent")
 def _(a):
     a.st(4, 10, -4, 1).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)

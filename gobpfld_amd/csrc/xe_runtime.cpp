@@ -896,6 +896,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (occ < 0) occ = blocks_per_cu(jit, P.nmaps);
     vm->last_grid = grid_blocks(n, occ, vm->cus);
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+  }
+  vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
+  if (mode != XE_MODE_SEQUENTIAL) {
     // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
@@ -903,7 +906,6 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         return fail(vm, XE_ERR_DEVICE, "replica fold");
     }
   }
-  vm->t1.rec(s);
   std::vector<unsigned long long> aux(aux_used);
   // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
   auto reduce = [&](std::vector<unsigned long long>& sum) {

@@ -46,35 +46,81 @@ ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
 ISSUE_PEAK = 256 * 64 * 2.4e9  # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz (SURVEY §8d issue roofline)
 
 
-def cpu_baseline(name: str, n_sample: int, target_s: float = 15.0) -> dict:
-    """The oracle (C++ restatement of emulator/, one thread) timed on a bounded prefix of the workload.
-
-    n_sample = 0 calibrates on a 20k-packet prefix and then times a prefix sized for ~target_s seconds."""
+def _oracle_prep(name: str, start: int, n: int):
+    """A private oracle VM loaded with `name` and the host batch of packets [start, start+n)."""
     from gobpfld_amd import _native as N
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
+    vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
+    W.setup_vm(vm, name)
+    umem, descs = W.build_batch(name, start, n)
+    return vm, umem, descs
+
+
+def _oracle_run(job) -> float:
+    """insns/pkt of one prepared shard (ctypes releases the GIL: threads run in parallel)."""
+    vm, umem, descs = job
+    r = vm.run_batch(umem, descs)
+    vm.close()
+    return r.stats["steps"] / max(1, len(descs))
+
+
+def _oracle_rate(name: str, start: int, n: int) -> tuple[float, float]:
+    job = _oracle_prep(name, start, n)
+    t0 = time.perf_counter()
+    ipp = _oracle_run(job)
+    return time.perf_counter() - t0, ipp
+
+
+def cpu_baseline(name: str, n_sample: int, target_s: float = 12.0, threads: int = 0) -> dict:
+    """The oracle (C++ restatement of emulator/) timed on a bounded prefix of the workload: one thread,
+    then `threads` threads, each a private VM over a contiguous shard (valid: the configs' map
+    effects commute), wall clock over the whole sample.
+
+    n_sample = 0 calibrates on a 20k-packet prefix and sizes the sample for ~target_s seconds."""
+    from concurrent.futures import ThreadPoolExecutor
     from gobpfld_amd import build as B
     B.build_oracle()
-    vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
-    if not n_sample:
-        W.setup_vm(vm, name)
-        cu, cd = W.build_batch(name, 0, 20_000)
+    threads = threads or min(16, os.cpu_count() or 1)
+    cal_dt, _ = _oracle_rate(name, 0, 20_000)
+    r1 = 20_000 / cal_dt
+    n1 = n_sample or int(min(max(r1 * target_s / 2, 50_000), 8_000_000))
+    dt1, ipp = _oracle_rate(name, 0, n1)
+    nt = n_sample or int(min(max(r1 * threads * target_s / 2, 50_000), 32_000_000))
+    per = (nt + threads - 1) // threads
+    with ThreadPoolExecutor(threads) as ex:
+        jobs = list(ex.map(lambda k: _oracle_prep(name, k * per, per), range(threads)))
         t0 = time.perf_counter()
-        vm.run_batch(cu, cd)
-        rate = 20_000 / (time.perf_counter() - t0)
-        n_sample = int(min(max(rate * target_s, 50_000), 8_000_000))
-        vm.close()
-        vm = VM(Settings(), lib=N.Lib(ROOT / "oracle" / "liboracle.so", "orc_"))
-    W.setup_vm(vm, name)
-    umem, descs = W.build_batch(name, 0, n_sample)
+        list(ex.map(_oracle_run, jobs))
+        dtt = time.perf_counter() - t0
+    return {"value": round(per * threads / dtt / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(n1 / dt1 / 1e6, 4),
+            "sample": f"{per * threads} packets of {name} on {threads} threads (private VMs on contiguous shards, "
+                      f"{dtt:.2f} s wall) and the first {n1} packets on 1 thread ({dt1:.2f} s) through "
+                      f"oracle/liboracle.so (C++ restatement of gobpfld emulator/, per-packet Reset/Run harness); "
+                      f"{ipp:.1f} insns/pkt"}
+
+
+def e2e_baseline(vm, umem: np.ndarray, descs: np.ndarray, iters: int = 3) -> dict:
+    """End-to-end rate: packets start and end in host memory. Pinned host UMEM + descriptors ->
+    hipMemcpyAsync H2D -> emulator kernel -> D2H verdicts (+ packet bytes when the program can write
+    them) through xe_run_batch_host. Never `value`; reported beside it."""
+    import torch
+    n = len(descs)
+    pu = torch.from_numpy(umem).pin_memory()
+    pd = torch.from_numpy(descs.view(np.uint8)).pin_memory()
+    pv = torch.empty(n, dtype=torch.int32).pin_memory()
+    args = (pu.data_ptr(), pu.numel(), pd.data_ptr(), n, pv.data_ptr())
+    vm.run_batch_host_ptrs(*args)  # warm-up (device staging buffers)
     t0 = time.perf_counter()
-    r = vm.run_batch(umem, descs)
-    dt = time.perf_counter() - t0
-    vm.close()
-    return {"value": round(n_sample / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-            "sample": f"first {n_sample} packets of {name} through oracle/liboracle.so (C++ restatement of "
-                      f"gobpfld emulator/, single thread, per-packet Reset/Run harness); {dt:.2f} s; "
-                      f"{r.stats['steps'] / n_sample:.1f} insns/pkt"}
+    for _ in range(iters):
+        st = vm.run_batch_host_ptrs(*args)
+    dt = (time.perf_counter() - t0) / iters
+    h2d = pu.numel() + pd.numel()
+    return {"value": round(n / dt / 1e6, 3), "unit": "Mpkt/s", "ms_per_batch": round(dt * 1e3, 3),
+            "device_ms_per_batch": round(st["total_ms"], 3), "h2d_bytes_per_packet": round(h2d / n, 2),
+            "d2h_bytes_per_packet": 4, "packets": n,
+            "path": "pinned host UMEM + descriptors -> H2D -> kernel -> D2H verdicts (xe_run_batch_host)"}
 
 
 def main() -> None:
@@ -87,6 +133,7 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=0, help="oracle baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", default="auto", choices=["auto", "interp", "jit"])
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     args = ap.parse_args()
 
     import torch
@@ -115,7 +162,6 @@ def main() -> None:
     d_umem = torch.from_numpy(umem).to(dev)
     d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
-    del umem
 
     engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
     vm = VM(Settings(device=local, engine=engine))
@@ -168,6 +214,10 @@ def main() -> None:
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     insns_per_pkt = steps_retired / max(1, n * args.steps)
 
+    e2e = None
+    if rank == 0 and not args.no_e2e:
+        e2e = e2e_baseline(vm, umem, descs)
+    del umem
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
@@ -199,6 +249,7 @@ def main() -> None:
                          "alg_bytes_per_packet": ALG_DESC.get(name, "16 desc + min(len,64) header + 4 verdict"),
                          "issue_frac": round(insns_per_pkt * n / avg_kernel_s / ISSUE_PEAK, 5)},
             "cpu_baseline": cpu,
+            "e2e": e2e,
         }
         print(json.dumps(out), flush=True)
     vm.close()

@@ -987,7 +987,7 @@ int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc
   if ((results && d2h(results, vm->d_res, size_t(n) * sizeof(xe_result), s)) ||
       (verdicts && d2h(verdicts, vm->d_ver, size_t(n) * 4, s)) ||
       (regs && d2h(regs, vm->d_regs, size_t(n) * sizeof(xe_regs), s)) ||
-      (umem_len && d2h(umem, vm->d_umem, umem_len, s)))
+      (umem_len && may_write_packet(vm->programs[vm->entry]) && d2h(umem, vm->d_umem, umem_len, s)))
     return fail(vm, XE_ERR_DEVICE, "D2H");
   b.rec(s);
   if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");

@@ -188,6 +188,15 @@ class VM:
         self._check(rc, "run batch")
         return BatchResult(res, ver, regs, _stats_dict(st))
 
+    def run_batch_host_ptrs(self, umem: int, umem_len: int, desc: int, n: int, verdicts: int = 0,
+                            results: int = 0) -> dict:
+        """Host-memory batch over caller-owned (ideally pinned) buffers given as addresses."""
+        st = N.BatchStats()
+        rc = self.lib.run_batch_host(self.h, umem or None, umem_len, desc or None, n, results or None,
+                                     verdicts or None, None, C.byref(st))
+        self._check(rc, "run batch (host pointers)")
+        return _stats_dict(st)
+
     def run_batch_device(self, d_umem: int, umem_len: int, d_desc: int, n: int, d_results: int = 0,
                          d_verdicts: int = 0, d_regs: int = 0, stream: int = 0) -> dict:
         """Device-resident batch: all pointers are device addresses (e.g. torch tensor .data_ptr())."""

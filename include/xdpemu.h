@@ -222,7 +222,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
                         void* d_results, void* d_verdicts, void* d_regs, void* stream,
                         xe_batch_stats* stats);
 /* Host-memory form (end-to-end: pinned staging + hipMemcpyAsync H2D/D2H). Packet writes made by the
- * program are copied back into umem. results/regs may be NULL. */
+ * program are copied back into umem (only when the program can write packet memory at all: a
+ * may-point-to analysis of the program at load). results/regs may be NULL. */
 int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* desc, uint32_t n,
                       xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);
 

@@ -99,6 +99,21 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_FP_MAPS 4
 #endif
 
+// Register class masks: what a register may hold at an instruction, computed by the per-program
+// kernel generator (xe_jit.cpp, a forward union dataflow over the program). Handlers take the mask
+// of the registers they dereference and skip the branches of impossible classes; the interpreter
+// passes XE_CM_ALL. XE_CM_ALIAS: the register may alias an object stored in a ValueMemory.
+#define XE_CM_IMM 1u
+#define XE_CM_PKT 2u
+#define XE_CM_CTX 4u
+#define XE_CM_STACK 8u
+#define XE_CM_ARRAY 16u
+#define XE_CM_HASH 32u
+#define XE_CM_ALIAS 64u
+#define XE_CM_VM (XE_CM_CTX | XE_CM_STACK)
+#define XE_CM_MAPS (XE_CM_ARRAY | XE_CM_HASH)
+#define XE_CM_ALL 127u
+
 // Packet header window staged in LDS per lane (the first 64 bytes are the hot bytes).
 // The window is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR destination) from the 16-byte
 // aligned address below the packet start, as XE_HDR_ROWS rows of 16 bytes per lane; one DMA
@@ -350,13 +365,13 @@ XE_DEV void alias_refresh(XeLane& L, uint32_t a, int64_t v) {
 }
 
 // RegisterValue.Assign on register d's object (in place; registers.go:194-197,243-247,305-313)
-XE_DEV int reg_inplace(XeLane& L, int d, int64_t v) {
+XE_DEV int reg_inplace(XeLane& L, int d, int64_t v, uint32_t cm = XE_CM_ALL) {
   XeReg r = reg_get(L, d);
   if (XE_T_KIND(r.t) == XE_KIND_FRAMEPTR && (r.t & XE_T_RO)) return XE_E_READONLY;
   r.v = v;
   reg_put(L, d, r);
   uint32_t a = XE_T_ALIAS(r.t);
-  if (a) {
+  if ((cm & XE_CM_ALIAS) && a) {
     obj_set_val(L, int(a), v);
     alias_refresh(L, a, v);
   }
@@ -691,9 +706,9 @@ XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
 // ------------------------------------------------------------------ generic memory ops
 // Memory.Read for either kind. Outputs the RegisterValue to put in a register.
 XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size, bool track,
-                    uint32_t& kind, uint32_t& oh, int64_t& val, uint32_t& alias) {
+                    uint32_t& kind, uint32_t& oh, int64_t& val, uint32_t& alias, uint32_t cm = XE_CM_ALL) {
   uint32_t c = xe_h_cls(h);
-  if (c == XE_H_CTX || c == XE_H_STACK) {
+  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
     int id = 0;
     if (int e = vmem_read(L, h, off, size, id)) return e;
     uint32_t t;
@@ -702,7 +717,7 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
     alias = (uint32_t(id) << 8) | (t & XE_T_RO);
     return 0;
   }
-  if (c == XE_H_PKT) {
+  if ((cm & XE_CM_PKT) && c == XE_H_PKT) {
     if (int e = bounds(off, size, L.plen)) return e;
     val = int64_t(pkt_load(L, off, size));
     kind = XE_KIND_IMM;
@@ -710,6 +725,7 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
     alias = 0;
     return 0;
   }
+  if (!(cm & XE_CM_MAPS)) return XE_EV_UNSUP;  // excluded by the class analysis (never reached)
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
@@ -723,9 +739,9 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
 
 // Memory.Write of a new object {kind, oh, val} (ST: new IMM; STX: Copy of src)
 XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size,
-                     uint32_t kind, uint32_t oh, int64_t val) {
+                     uint32_t kind, uint32_t oh, int64_t val, uint32_t cm = XE_CM_ALL) {
   uint32_t c = xe_h_cls(h);
-  if (c == XE_H_CTX || c == XE_H_STACK) {
+  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
     int wb; int64_t len;
     vmem_region(h, wb, len);
     if (int e = bounds(off, size, len)) return e;
@@ -735,11 +751,12 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
     vmem_fill(L, wb, off, size, id);
     return 0;
   }
-  if (c == XE_H_PKT) {
+  if ((cm & XE_CM_PKT) && c == XE_H_PKT) {
     if (int e = bounds(off, size, L.plen)) return e;
     pkt_store(L, off, size, uint64_t(val));
     return 0;
   }
+  if (!(cm & XE_CM_MAPS)) return XE_EV_UNSUP;  // excluded by the class analysis (never reached)
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
@@ -751,43 +768,51 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
 // PointerValue.ReadRange (registers.go:218-220,273-281; memory.go:55-95,176-185).
 // emit(i, byte) receives the output bytes. Returns 0 / XE_E_OOB / panic. dry = validate only.
 template <class Emit>
-XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Emit emit) {
+XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Emit emit, uint32_t cm = XE_CM_ALL) {
   const XeReg R = reg_get(L, r);
   uint32_t kind = XE_T_KIND(R.t);
   uint32_t h = R.h;
   int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R.v) : R.v;
   uint32_t c = xe_h_cls(h);
-  if (c == XE_H_CTX || c == XE_H_STACK) {
+  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
     int wb; int64_t len;
     vmem_region(h, wb, len);
     if (off < 0 || xe_wadd(off, count) > len) return XE_E_OOB;
     if (off >= len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
+    // Byte groups of equal object references, each written 1/2/4/8 bytes wide (memory.go:61-91).
+    // Written as fixed-trip loops (skip counts the bytes a wide write already produced) so that a
+    // per-program kernel with a constant count unrolls it fully and folds the object ids.
+    int skip = 0;
     XE_UNROLL_VM
-    for (int64_t i = 0; i < count;) {
-      int v = vmem_byte(L, wb, off + i);
-      if (!v) { emit(i, 0); i++; continue; }
+    for (int64_t i = 0; i < count; i++) {
+      if (skip > 0) { skip--; continue; }
+      const int v = vmem_byte(L, wb, off + i);
+      if (!v) { emit(i, 0); continue; }
       int size = 1;
+      bool run = true;
       XE_UNROLL_VM
-      for (int64_t j = i + 1; j < i + 8 && j < count; j++) {
-        if (vmem_byte(L, wb, off + j) != v) break;
-        size++;
+      for (int j = 1; j < 8; j++) {
+        run = run && i + j < count && vmem_byte(L, wb, off + i + j) == v;
+        size += run ? 1 : 0;
       }
-      int w = size > 4 ? 8 : size > 2 ? 4 : size > 1 ? 2 : 1;
+      const int w = size > 4 ? 8 : size > 2 ? 4 : size > 1 ? 2 : 1;
       if (i + w > count) return XE_EV_PANIC | XE_P_INDEX;
       int64_t ov; uint32_t oh, ot;
       obj_get(L, v, ov, oh, ot);
       XE_UNROLL_VM
-      for (int b = 0; b < w; b++) emit(i + b, uint8_t(uint64_t(ov) >> (8 * b)));
-      i += w;
+      for (int b = 0; b < 8; b++)
+        if (b < w) emit(i + b, uint8_t(uint64_t(ov) >> (8 * b)));
+      skip = w - 1;
     }
     return 0;
   }
-  if (c == XE_H_PKT) {
+  if ((cm & XE_CM_PKT) && c == XE_H_PKT) {
     if (off < 0 || xe_wadd(off, count) > L.plen) return XE_E_OOB;
 #pragma unroll 1
     for (int64_t i = 0; i < count; i++) emit(i, uint8_t(pkt_load(L, off + i, 1)));
     return 0;
   }
+  if (!(cm & XE_CM_MAPS)) return XE_EV_UNSUP;  // excluded by the class analysis (never reached)
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
@@ -838,11 +863,12 @@ XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty
 
 // read a key through a pointer register into zero-padded words; ReadRange errors give the nil key
 // (maps_hash.go:50-53). Returns a panic code or 0.
-XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint64_t* kw, bool& empty) {
+XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint64_t* kw, bool& empty,
+                    uint32_t cm = XE_CM_ALL) {
   for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
   int e = ptr_read_range(L, P, r, int64_t(M.key_size), [&](int64_t i, uint8_t b) {
     kw[i >> 3] |= uint64_t(b) << (8 * (i & 7));
-  });
+  }, cm);
   if (XE_IS_PANIC(e)) return e;
   empty = e != 0 || M.key_size == 0;
   if (empty)
@@ -852,12 +878,12 @@ XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint
 
 // ------------------------------------------------------------------ helpers
 // regToMap, helper_functions.go:109-130. m = 0 means "R0 := 0, helper returns nil".
-XE_DEV int reg_to_map(XeLane& L, const XeParams& P, uint32_t& m) {
+XE_DEV int reg_to_map(XeLane& L, const XeParams& P, uint32_t& m, uint32_t cm1 = XE_CM_ALL) {
   const XeReg R1 = reg_get(L, 1);
   int64_t idx = R1.v;
-  if (XE_T_KIND(R1.t) == XE_KIND_MEMPTR) {
+  if ((cm1 & ~(XE_CM_IMM | XE_CM_ALIAS)) && XE_T_KIND(R1.t) == XE_KIND_MEMPTR) {
     uint32_t k, oh, al; int64_t v;
-    if (int e = mem_read(L, P, R1.h, R1.v, 4, true, k, oh, v, al)) return e;
+    if (int e = mem_read(L, P, R1.h, R1.v, 4, true, k, oh, v, al, cm1)) return e;
     idx = v;
   }
   if (idx < 1 || idx > int64_t(P.nmaps)) {
@@ -875,9 +901,9 @@ XE_DEV int helper_errno_result(XeLane& L, int64_t v) {
 }
 
 // MapLookupElement, helper_functions.go:46-73
-XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
+XE_DEV int helper_lookup(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL) {
   uint32_t m;
-  if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (int e = reg_to_map(L, P, m, cm1)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
   const XeDevMap M = map_desc(L, m);
   const XeReg R2 = reg_get(L, 2);
@@ -886,7 +912,7 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
     uint32_t kind = XE_T_KIND(R2.t);
     int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R2.v) : R2.v;
     uint32_t k, oh, al; int64_t kv;
-    int e = mem_read(L, P, R2.h, off, 4, true, k, oh, kv, al);
+    int e = mem_read(L, P, R2.h, off, 4, true, k, oh, kv, al, cm2);
     if (XE_IS_PANIC(e)) return e;
     if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;  // error ignored, nil keyValReg.Value()
     int64_t voff = xe_wmul(kv, int64_t(M.value_size));
@@ -897,7 +923,7 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
   if (XE_HAS_HASH && M.kind == XE_DM_HASH) {  // HashMap.Lookup, maps_hash.go:44-63
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = read_key(L, P, 2, M, kw, empty)) return e;
+    if (int e = read_key(L, P, 2, M, kw, empty, cm2)) return e;
     int64_t slot = hash_find(M, kw, empty);
     if (slot < 0) reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
     else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), 0, 0);
@@ -907,9 +933,10 @@ XE_DEV int helper_lookup(XeLane& L, const XeParams& P) {
 }
 
 // MapUpdateElement, helper_functions.go:76-101
-XE_DEV int helper_update(XeLane& L, const XeParams& P) {
+XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
+                         uint32_t cm3 = XE_CM_ALL) {
   uint32_t m;
-  if (int e = reg_to_map(L, P, m)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (int e = reg_to_map(L, P, m, cm1)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
   if (!m) return 0;
   const XeDevMap M = map_desc(L, m);
   if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
@@ -917,13 +944,13 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
     if (XE_T_KIND(R3.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     if (XE_T_KIND(R2.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     uint32_t k, oh, al; int64_t kv;
-    if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al))
+    if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al, cm2))
       return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
     if (kv >= int64_t(M.vals_bytes)) return helper_errno_result(L, -7);
 #pragma unroll 1
     for (int64_t i = 0; i < int64_t(M.value_size); i++) {
       int64_t v;
-      if (int e = mem_read(L, P, R3.h, i, 1, true, k, oh, v, al))  // ignores the value ptr offset
+      if (int e = mem_read(L, P, R3.h, i, 1, true, k, oh, v, al, cm3))  // ignores the value ptr offset
         return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
       int64_t dst = xe_wadd(xe_wmul(kv, int64_t(M.value_size)), i);
       if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
@@ -936,12 +963,12 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
     if (XE_T_KIND(reg_get(L, 2).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = read_key(L, P, 2, M, kw, empty)) return e;
+    if (int e = read_key(L, P, 2, M, kw, empty, cm2)) return e;
     int64_t slot = hash_find(M, kw, empty);
     if (slot < 0 && uint64_t(*M.count) + 1 > M.max_entries) return helper_errno_result(L, -7);
     if (XE_T_KIND(reg_get(L, 3).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
     // value ReadRange: validate first (a panic must leave the map untouched)
-    int ve = ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t, uint8_t) {});
+    int ve = ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
     if (XE_IS_PANIC(ve)) return ve;
     if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
     if (slot < 0) slot = hash_insert_new(M, kw, empty);
@@ -950,19 +977,20 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P) {
       M.state[slot] |= XE_SLOT_VLEN0;  // nil backing
     } else {
       M.state[slot] &= ~XE_SLOT_VLEN0;
-      ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; });
+      ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; }, cm3);
     }
     return helper_errno_result(L, 0);
   }
   return XE_EV_UNSUP;
 }
 
-XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn) {
+XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
+                       uint32_t cm3 = XE_CM_ALL) {
   if (fn >= 192) return XE_E_NO_HELPER;
   if (fn < 0) return XE_EV_PANIC | XE_P_INDEX;
   switch (fn) {
-    case 1: return helper_lookup(L, P);
-    case 2: return helper_update(L, P);
+    case 1: return helper_lookup(L, P, cm1, cm2);
+    case 2: return helper_update(L, P, cm1, cm2, cm3);
     case 3: return XE_E_NOT_IMPL | XE_E_IN_HELPER;
     case 14: reg_replace(L, 0, XE_KIND_IMM, 0, (int64_t(1234) << 32) + 5678, 0); return 0;
     case 12: case 25: case 87: case 88: case 89: return XE_EV_UNSUP;
@@ -1055,7 +1083,7 @@ XE_DEV int64_t ptr_eff(const XeReg& R, int32_t ioff) {
 }
 
 // ---- per-class handlers (exec_uop dispatches; the JIT calls them directly with constant uops)
-XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u) {
+XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const int d = u.dst, s = u.src;
   const bool wide = u.fl & UF_WIDE, reg = u.fl & UF_REG;
   const XeReg D = reg_get(L, d);
@@ -1069,7 +1097,7 @@ XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u) {
   if ((u.x == 0x30 || u.x == 0x90) && S.v == 0) return XE_E_DIV0;
   int64_t v;
   if (int e = alu_compute(u.x, wide, D.v, S.v, v)) return e;
-  return reg_inplace(L, d, v);
+  return reg_inplace(L, d, v, cmd);
 }
 
 XE_DEV int uop_movi(XeLane& L, const XeUop& u) {
@@ -1083,13 +1111,13 @@ XE_DEV int uop_movr(XeLane& L, const XeUop& u) {
   return 0;
 }
 
-XE_DEV int uop_neg(XeLane& L, const XeUop& u) {
+XE_DEV int uop_neg(XeLane& L, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const int64_t dv = reg_get(L, u.dst).v;
   int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(xe_i32(dv))));
-  return reg_inplace(L, u.dst, v);
+  return reg_inplace(L, u.dst, v, cmd);
 }
 
-XE_DEV int uop_end(XeLane& L, const XeUop& u) {
+XE_DEV int uop_end(XeLane& L, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   uint64_t rv = uint64_t(reg_get(L, u.dst).v), v;
   if (u.x == 0) {
     v = u.imm == 16 ? uint64_t(__builtin_bswap16(uint16_t(rv)))
@@ -1097,7 +1125,7 @@ XE_DEV int uop_end(XeLane& L, const XeUop& u) {
   } else {
     v = u.imm == 16 ? uint64_t(uint16_t(rv)) : u.imm == 32 ? uint64_t(uint32_t(rv)) : rv;
   }
-  return reg_inplace(L, u.dst, int64_t(v));
+  return reg_inplace(L, u.dst, int64_t(v), cmd);
 }
 
 // returns whether the branch is taken
@@ -1115,7 +1143,7 @@ XE_DEV bool uop_jmp(const XeLane& L, const XeUop& u) {
   return u.x == 0x50 ? (!imm || c) : (imm && c);
 }
 
-XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u) {
+XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const int d = u.dst, s = u.src;
   if (s == 1) { reg_replace(L, d, XE_KIND_IMM, 0, int64_t(uint32_t(u.imm)), 0); return 0; }
   if (s == 2) {  // BPF_PSEUDO_MAP_FD_VALUE, inst_load.go:36-63
@@ -1138,36 +1166,36 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u) {
     }
     return XE_EV_UNSUP;
   }
-  return reg_inplace(L, d, int64_t((uint64_t(u.x) << 32) + uint64_t(uint32_t(u.imm))));
+  return reg_inplace(L, d, int64_t((uint64_t(u.x) << 32) + uint64_t(uint32_t(u.imm))), cmd);
 }
 
-XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u) {
+XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cms = XE_CM_ALL) {
   const XeReg S = reg_get(L, u.src);
-  if (XE_T_KIND(S.t) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
+  if ((cms & XE_CM_IMM) && XE_T_KIND(S.t) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
   uint32_t kind, oh, al; int64_t v;
-  if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), true, kind, oh, v, al)) return e;
+  if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), true, kind, oh, v, al, cms)) return e;
   if (u.fl & UF_BADDST) return XE_E_ASSIGN_REG;
   reg_replace(L, u.dst, kind, oh, v, al);
   return 0;
 }
 
 // ST (u.cls == U_ST, value = imm) and STX
-XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u) {
+XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const XeReg D = reg_get(L, u.dst);
-  if (XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
   const bool st = u.cls == U_ST;
   const XeReg S = st ? XeReg{int64_t(u.imm), 0, uint32_t(XE_KIND_IMM)} : reg_get(L, u.src);
-  return mem_write(L, P, D.h, ptr_eff(D, u.tgt), uop_size(u), XE_T_KIND(S.t), S.h, S.v);
+  return mem_write(L, P, D.h, ptr_eff(D, u.tgt), uop_size(u), XE_T_KIND(S.t), S.h, S.v, cmd);
 }
 
-XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
+XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const XeReg D = reg_get(L, u.dst);
-  if (XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
   const uint32_t h = D.h;
   const int64_t off = ptr_eff(D, u.tgt);
   const int size = uop_size(u);
   const uint32_t c = xe_h_cls(h);
-  if (c == XE_H_CTX || c == XE_H_STACK) {
+  if ((cmd & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
     int id = 0;
     if (int e = vmem_read(L, h, off, size, id)) return e;
     if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
@@ -1179,12 +1207,13 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
     alias_refresh(L, uint32_t(id), nv);
     return 0;
   }
-  if (c == XE_H_PKT) {
+  if ((cmd & XE_CM_PKT) && c == XE_H_PKT) {
     if (int e = bounds(off, size, L.plen)) return e;
     if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
     pkt_store(L, off, size, pkt_load(L, off, size) + uint64_t(reg_get(L, u.src).v));
     return 0;
   }
+  if (!(cmd & XE_CM_MAPS)) return XE_EV_UNSUP;  // excluded by the class analysis (never reached)
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
@@ -1195,8 +1224,9 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u) {
   return 0;
 }
 
-XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u) {
-  return call_helper(L, P, u.cls == U_HELPER ? int64_t(u.imm) : reg_get(L, u.dst).v);
+XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
+                      uint32_t cm3 = XE_CM_ALL) {
+  return call_helper(L, P, u.cls == U_HELPER ? int64_t(u.imm) : reg_get(L, u.dst).v, cm1, cm2, cm3);
 }
 
 // ------------------------------------------------------------------ one instruction

@@ -46,6 +46,19 @@ ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
 ISSUE_PEAK = 256 * 64 * 2.4e9  # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz (SURVEY §8d issue roofline)
 
 
+def pmc_traffic(name: str, n: int) -> tuple[float | None, str | None]:
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE x2 per
+    the gfx950 correction + WRITE_SIZE; profiles/r1/<config>_traffic.json, made by
+    scripts/pmc_traffic.py), when one exists for this exact batch size; else (None, None)."""
+    f = ROOT / "profiles" / "r1" / f"{name}_traffic.json"
+    if not f.exists():
+        return None, None
+    d = json.loads(f.read_text())
+    if d.get("workload") != name or int(d.get("packets", -1)) != n:
+        return None, None
+    return float(d["hbm_bytes_per_launch"]), str(f.relative_to(ROOT))
+
+
 def _oracle_prep(name: str, start: int, n: int):
     """A private oracle VM loaded with `name` and the host batch of packets [start, start+n)."""
     from gobpfld_amd import _native as N
@@ -213,6 +226,7 @@ def main() -> None:
     bytes_per_launch = float(alg_bytes_per_packet(name, sizes).sum())
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
     insns_per_pkt = steps_retired / max(1, n * args.steps)
+    traffic, traffic_src = pmc_traffic(name, n)
 
     e2e = None
     if rank == 0 and not args.no_e2e:
@@ -243,7 +257,8 @@ def main() -> None:
                        "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps),
                        "grid": grid},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+                         "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                          "kernel": "xe_jit_kernel" if engines == {"jit"} else "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "alg_bytes_per_packet": ALG_DESC.get(name, "16 desc + min(len,64) header + 4 verdict"),

@@ -12,7 +12,7 @@ tail -1 $OUT/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_kt.log 2>&1 || { echo kt failed; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || { echo fetch failed; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || { echo write failed; exit 1; }
-for c in c3 c4 c5; do
+for c in c1 c3 c4 c5; do
   timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -3 $OUT/bench_$c.log; exit 1; }
   tail -1 $OUT/bench_$c.log | cut -c1-300
 done

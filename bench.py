@@ -162,6 +162,7 @@ def main() -> None:
 
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import allreduce_map_deltas
 
     name = args.config
     n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))
@@ -180,17 +181,14 @@ def main() -> None:
     vm = VM(Settings(device=local, engine=engine))
     W.setup_vm(vm, name)
     maps = list(vm.map_defs)
-    deltas = {m: torch.zeros(vm.map_values_bytes(m) // 8, dtype=torch.int64, device=dev) for m in maps}
+    deltas = {m: torch.zeros(vm.map_values_bytes(m), dtype=torch.uint8, device=dev) for m in maps}
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step() -> dict:
         st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
                                  d_verdicts=d_ver.data_ptr(), stream=stream)
-        if world > 1:
-            for m in maps:  # counter deltas -> RCCL all-reduce (sum, u64 wrap) -> every replica
-                vm.map_delta(m, deltas[m].data_ptr(), stream=stream)
-                dist.all_reduce(deltas[m])
-                vm.map_apply_delta(m, deltas[m].data_ptr(), stream=stream)
+        if world > 1:  # map-value deltas -> one RCCL all-reduce per map -> every replica
+            allreduce_map_deltas(vm, maps, deltas, dist, stream=stream)
         return st
 
     for _ in range(args.warmup):

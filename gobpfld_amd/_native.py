@@ -75,8 +75,9 @@ _SIGS = {
     "run_batch_host": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),
     "run_batch_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
     "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
-    "map_delta": (C.c_int, [P, C.c_int32, P, P]),
-    "map_apply_delta": (C.c_int, [P, C.c_int32, P, P]),
+    "map_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
+    "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
+    "map_delta_lane": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint32)]),
     "footprint": (C.c_int, [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
     "version": (C.c_char_p, []),
     "device_count": (C.c_int, [C.POINTER(C.c_int)]),
@@ -88,7 +89,7 @@ HEADER_SYMBOLS = [
     "xe_default_settings", "xe_create", "xe_destroy", "xe_last_error", "xe_add_raw_program",
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
     "xe_map_count", "xe_map_dump", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
-    "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_footprint", "xe_version",
+    "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
     "xe_device_count",
 ]
 

@@ -28,29 +28,53 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   flush_wave_state(L, P);
 }
 
-extern "C" __global__ void xe_delta_kernel(const unsigned long long* cur, const unsigned long long* snap,
-                                           unsigned long long* out, uint64_t nwords) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x)
-    out[i] = cur[i] - snap[i];
+// Map-value deltas for the multi-GPU reduction, lane-wise at the width of the map's adds (T): a
+// narrow counter wraps at its own width, so a u64 word difference would borrow across fields.
+template <class T>
+__global__ void xe_delta_kernel(const T* cur, const T* snap, T* out, uint64_t n) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    out[i] = T(cur[i] - snap[i]);
+}
+template <class T>
+__global__ void xe_apply_delta_kernel(T* cur, const T* snap, const T* delta, uint64_t n) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    cur[i] = T(snap[i] + delta[i]);
 }
 
-extern "C" __global__ void xe_apply_delta_kernel(unsigned long long* cur, const unsigned long long* snap,
-                                                 const unsigned long long* delta, uint64_t nwords) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x)
-    cur[i] = snap[i] + delta[i];
-}
-
-// vals += sum of the replicas; replicas := 0 (only words that received adds are written)
-extern "C" __global__ void xe_rep_fold_kernel(unsigned long long* vals, unsigned long long* rep, uint64_t stride_words,
-                                              uint32_t nrep, uint64_t nwords) {
+// vals += sum of the replicas; replicas := 0 (only words that received adds are written). All nrep
+// loads are issued before any store so they overlap (no store may alias a later load).
+extern "C" __global__ void xe_rep_fold_kernel(unsigned long long* __restrict__ vals, unsigned long long* __restrict__ rep,
+                                              uint64_t stride_words, uint32_t nrep, uint64_t nwords) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x) {
+    unsigned long long v[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) v[k] = k < nrep ? rep[k * stride_words + i] : 0ull;
     unsigned long long s = 0;
-    for (uint32_t k = 0; k < nrep; k++) {
-      const unsigned long long v = rep[k * stride_words + i];
-      if (v) { s += v; rep[k * stride_words + i] = 0; }
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      s += v[k];
+      if (v[k]) rep[k * stride_words + i] = 0;
     }
     if (s) vals[i] += s;
   }
+}
+
+// Run prologue in one launch: snapshot up to XE_PRO_SEGS map value regions (u64 words) and zero the
+// statistics / flag words (replaces a copy per map plus a fill: each costs a launch).
+#define XE_PRO_SEGS 8
+struct XeProlog {
+  const unsigned long long* src[XE_PRO_SEGS];
+  unsigned long long* dst[XE_PRO_SEGS];
+  uint64_t words[XE_PRO_SEGS];
+  uint32_t nseg;
+  unsigned long long* zero;
+  uint64_t zero_words;
+};
+extern "C" __global__ void xe_prologue_kernel(XeProlog A) {
+  const uint64_t tid = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x, nth = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = tid; i < A.zero_words; i += nth) A.zero[i] = 0;
+  for (uint32_t g = 0; g < A.nseg; g++)
+    for (uint64_t i = tid; i < A.words[g]; i += nth) A.dst[g][i] = A.src[g][i];
 }
 
 // host-side launchers (called from xe_runtime.cpp)
@@ -64,24 +88,64 @@ extern "C" int xe_interp_occupancy(uint32_t nmaps) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, xe_interp_kernel, 256, (nmaps + 1) * sizeof(XeDevMap)) != hipSuccess) return 0;
   return nb;
 }
-extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s) {
-  uint32_t blocks = uint32_t(nwords / 256 + 1);
+template <class T>
+static int launch_delta_t(const void* cur, const void* snap, void* out, uint64_t n, hipStream_t s) {
+  uint32_t blocks = uint32_t(n / 256 + 1);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(xe_delta_kernel, dim3(blocks), dim3(256), 0, s, (const unsigned long long*)cur,
-                     (const unsigned long long*)snap, (unsigned long long*)out, nwords);
+  hipLaunchKernelGGL(xe_delta_kernel<T>, dim3(blocks), dim3(256), 0, s, (const T*)cur, (const T*)snap, (T*)out, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template <class T>
+static int launch_apply_t(void* cur, const void* snap, const void* delta, uint64_t n, hipStream_t s) {
+  uint32_t blocks = uint32_t(n / 256 + 1);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(xe_apply_delta_kernel<T>, dim3(blocks), dim3(256), 0, s, (T*)cur, (const T*)snap, (const T*)delta, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// bytes: length of the value region (multiple of 8); lane: 1, 2, 4 or 8
+extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, hipStream_t s) {
+  switch (lane) {
+    case 1: return launch_delta_t<uint8_t>(cur, snap, out, bytes, s);
+    case 2: return launch_delta_t<uint16_t>(cur, snap, out, bytes / 2, s);
+    case 4: return launch_delta_t<uint32_t>(cur, snap, out, bytes / 4, s);
+    default: return launch_delta_t<unsigned long long>(cur, snap, out, bytes / 8, s);
+  }
+}
+extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane,
+                                     hipStream_t s) {
+  switch (lane) {
+    case 1: return launch_apply_t<uint8_t>(cur, snap, delta, bytes, s);
+    case 2: return launch_apply_t<uint16_t>(cur, snap, delta, bytes / 2, s);
+    case 4: return launch_apply_t<uint32_t>(cur, snap, delta, bytes / 4, s);
+    default: return launch_apply_t<unsigned long long>(cur, snap, delta, bytes / 8, s);
+  }
+}
+extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
+                                  void* zero, uint64_t zero_words, hipStream_t s) {
+  for (uint32_t base = 0; base < nseg || base == 0; base += XE_PRO_SEGS) {
+    XeProlog A{};
+    A.nseg = nseg - base < XE_PRO_SEGS ? nseg - base : XE_PRO_SEGS;
+    uint64_t mx = base == 0 ? zero_words : 0;
+    for (uint32_t g = 0; g < A.nseg; g++) {
+      A.src[g] = (const unsigned long long*)src[base + g];
+      A.dst[g] = (unsigned long long*)dst[base + g];
+      A.words[g] = words[base + g];
+      if (A.words[g] > mx) mx = A.words[g];
+    }
+    A.zero = (unsigned long long*)zero;
+    A.zero_words = base == 0 ? zero_words : 0;
+    uint64_t blocks = (mx + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 4096 ? 4096 : blocks;
+    hipLaunchKernelGGL(xe_prologue_kernel, dim3(uint32_t(blocks)), dim3(256), 0, s, A);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (nseg == 0) break;
+  }
+  return 0;
 }
 extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s) {
   uint32_t blocks = uint32_t(nwords / 256 + 1);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(xe_rep_fold_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)vals, (unsigned long long*)rep,
                      stride_words, nrep, nwords);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s) {
-  uint32_t blocks = uint32_t(nwords / 256 + 1);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(xe_apply_delta_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)cur,
-                     (const unsigned long long*)snap, (const unsigned long long*)delta, nwords);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

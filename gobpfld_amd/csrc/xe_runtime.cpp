@@ -26,9 +26,12 @@ typedef void* xe_stream_t;
 #include <hip/hip_runtime_api.h>
 typedef hipStream_t xe_stream_t;
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
-extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t nwords, hipStream_t s);
-extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, hipStream_t s);
+extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane,
+                                     hipStream_t s);
 extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
+                                  void* zero, uint64_t zero_words, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
                             const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -65,12 +68,36 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   return 0;
 }
 int launch_jit(void*, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return launch_interp(P, b, t, s); }
-int launch_delta(const void* cur, const void* snap, void* out, uint64_t nw, xe_stream_t) {
-  for (uint64_t i = 0; i < nw; i++) ((uint64_t*)out)[i] = ((const uint64_t*)cur)[i] - ((const uint64_t*)snap)[i];
+template <class T>
+void lanes_sub(const void* a, const void* b, void* o, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) ((T*)o)[i] = T(((const T*)a)[i] - ((const T*)b)[i]);
+}
+template <class T>
+void lanes_add(const void* a, const void* b, void* o, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) ((T*)o)[i] = T(((const T*)a)[i] + ((const T*)b)[i]);
+}
+int launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, xe_stream_t) {
+  switch (lane) {
+    case 1: lanes_sub<uint8_t>(cur, snap, out, bytes); break;
+    case 2: lanes_sub<uint16_t>(cur, snap, out, bytes / 2); break;
+    case 4: lanes_sub<uint32_t>(cur, snap, out, bytes / 4); break;
+    default: lanes_sub<uint64_t>(cur, snap, out, bytes / 8); break;
+  }
   return 0;
 }
-int launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t nw, xe_stream_t) {
-  for (uint64_t i = 0; i < nw; i++) ((uint64_t*)cur)[i] = ((const uint64_t*)snap)[i] + ((const uint64_t*)delta)[i];
+int launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane, xe_stream_t) {
+  switch (lane) {
+    case 1: lanes_add<uint8_t>(snap, delta, cur, bytes); break;
+    case 2: lanes_add<uint16_t>(snap, delta, cur, bytes / 2); break;
+    case 4: lanes_add<uint32_t>(snap, delta, cur, bytes / 4); break;
+    default: lanes_add<uint64_t>(snap, delta, cur, bytes / 8); break;
+  }
+  return 0;
+}
+int launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg, void* zero, uint64_t zw,
+                    xe_stream_t) {
+  memset(zero, 0, zw * 8);
+  for (uint32_t g = 0; g < nseg; g++) memcpy(dst[g], src[g], words[g] * 8);
   return 0;
 }
 int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t) {
@@ -100,9 +127,17 @@ int dmemset(void* d, int v, size_t n, xe_stream_t s) { return hipMemsetAsync(d, 
 int dsync(xe_stream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -1; }
 int launch_interp(const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_launch_interp(P, b, t, s); }
 int launch_jit(void* fn, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return xe_jit_launch(fn, P, b, t, s); }
-int launch_delta(const void* c, const void* sn, void* o, uint64_t nw, xe_stream_t s) { return xe_launch_delta(c, sn, o, nw, s); }
-int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t nw, xe_stream_t s) { return xe_launch_apply_delta(c, sn, d, nw, s); }
+int launch_delta(const void* c, const void* sn, void* o, uint64_t b, uint32_t lane, xe_stream_t s) {
+  return xe_launch_delta(c, sn, o, b, lane, s);
+}
+int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t b, uint32_t lane, xe_stream_t s) {
+  return xe_launch_apply_delta(c, sn, d, b, lane, s);
+}
 int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t s) { return xe_launch_rep_fold(v, r, sw, nrep, nw, s); }
+int launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg, void* zero, uint64_t zw,
+                    xe_stream_t s) {
+  return xe_launch_prologue(src, dst, words, nseg, zero, zw, s);
+}
 struct Timer {
   hipEvent_t e = nullptr;
   void init() { if (!e) (void)hipEventCreate(&e); }
@@ -284,6 +319,7 @@ struct HostMap {
   uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
   uint32_t nrep = 1;
   uint64_t rep_stride = 0;
+  uint32_t lane = 0;  // width of the map adds of the last run (delta lanes): 0 none, 8 when mixed
   bool host_dirty = true, dev_dirty = false;
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -397,7 +433,7 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 // Replicas of the value region for deferred 8-byte adds (XeDevMap::rep): enough to spread a hot
 // counter's atomics, bounded in memory (HBM is plentiful, but every run folds all replicas).
 uint32_t choose_nrep(uint64_t vals_alloc) {
-  if (const char* e = getenv("XE_NREP")) return uint32_t(std::max(1, atoi(e)));  // tuning experiments
+  if (const char* e = getenv("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));  // tuning experiments
   return vals_alloc <= (8ull << 20) ? 16u : vals_alloc <= (64ull << 20) ? 8u : vals_alloc <= (256ull << 20) ? 4u : 1u;
 }
 
@@ -867,16 +903,25 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   auto launch = [&](const XeParams* p, uint32_t b, uint32_t t) {
     return jit ? launch_jit(jit, p, b, t, s) : launch_interp(p, b, t, s);
   };
-  // snapshot map values: rollback point for the ordered fallback and base of the shard deltas
-  for (size_t i = 1; i < vm->maps.size(); i++) {
-    HostMap& m = vm->maps[i];
-    if (d2d(m.d_snap, m.d_vals, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "snapshot");
+  // one prologue launch: snapshot the map values (rollback point for the ordered fallback and base of
+  // the shard deltas) and zero the statistics words
+  {
+    std::vector<const void*> src;
+    std::vector<void*> dst;
+    std::vector<uint64_t> words;
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      src.push_back(m.d_vals);
+      dst.push_back(m.d_snap);
+      words.push_back(m.vals_alloc / 8);
+    }
+    if (launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), vm->d_aux, aux_used, s))
+      return fail(vm, XE_ERR_DEVICE, "prologue");
   }
   // the ordered replay must also start from the original packet bytes
   const bool keep_pkts = mode == XE_MODE_AUTO && umem_len && may_write_packet(vm->programs[vm->entry]);
   if (keep_pkts && (ensure_buf(&vm->d_usnap, &vm->d_usnap_cap, umem_len) || d2d(vm->d_usnap, d_umem, umem_len, s)))
     return fail(vm, XE_ERR_DEVICE, "packet snapshot");
-  if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
   vm->t0.rec(s);
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
@@ -950,6 +995,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       kms += Timer::ms(vm->t1, vm->t2);
     }
   }
+  for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
+    const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
+    vm->maps[m].lane = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
+  }
   vm->last_flags = uint32_t(red[0]);
   vm->last_fp.assign(red.begin() + 16, red.end());
   for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
@@ -1003,22 +1052,33 @@ int xe_map_values_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
   return XE_OK;
 }
 
-int xe_map_delta(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
+int xe_map_delta(xe_vm* vm, int32_t mi, uint32_t lane, void* d_out, void* stream) {
   HostMap* m = get_map(vm, mi);
   if (!m || !d_out) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
-  if (launch_delta(m->d_vals, m->d_snap, d_out, m->vals_alloc / 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "delta");
+  if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
+  if (launch_delta(m->d_vals, m->d_snap, d_out, m->vals_alloc, lane ? lane : m->lane ? m->lane : 8, s) || dsync(s))
+    return fail(vm, XE_ERR_DEVICE, "delta");
   return XE_OK;
 }
 
-int xe_map_apply_delta(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
+int xe_map_apply_delta(xe_vm* vm, int32_t mi, uint32_t lane, const void* d_in, void* stream) {
   HostMap* m = get_map(vm, mi);
   if (!m || !d_in) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
-  if (launch_apply_delta(m->d_vals, m->d_snap, d_in, m->vals_alloc / 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "apply delta");
+  if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
+  if (launch_apply_delta(m->d_vals, m->d_snap, d_in, m->vals_alloc, lane ? lane : m->lane ? m->lane : 8, s) || dsync(s))
+    return fail(vm, XE_ERR_DEVICE, "apply delta");
   m->dev_dirty = true;
+  return XE_OK;
+}
+
+int xe_map_delta_lane(xe_vm* vm, int32_t mi, uint32_t* lane_bytes) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !lane_bytes) return XE_ERR_INVAL;
+  *lane_bytes = m->lane;
   return XE_OK;
 }
 

@@ -207,11 +207,17 @@ class VM:
         return _stats_dict(st)
 
     # ---- multi-GPU shard support
-    def map_delta(self, m: int, d_out: int, stream: int = 0) -> None:
-        self._check(self.lib.map_delta(self.h, m, d_out, stream or None), "map delta")
+    def map_delta(self, m: int, d_out: int, stream: int = 0, lane: int = 0) -> None:
+        self._check(self.lib.map_delta(self.h, m, lane, d_out, stream or None), "map delta")
 
-    def map_apply_delta(self, m: int, d_in: int, stream: int = 0) -> None:
-        self._check(self.lib.map_apply_delta(self.h, m, d_in, stream or None), "map apply delta")
+    def map_delta_lane(self, m: int) -> int:
+        """Lane width in bytes of map_delta / map_apply_delta (the width of the last run's map adds)."""
+        v = C.c_uint32()
+        self._check(self.lib.map_delta_lane(self.h, m, C.byref(v)), "map delta lane")
+        return v.value
+
+    def map_apply_delta(self, m: int, d_in: int, stream: int = 0, lane: int = 0) -> None:
+        self._check(self.lib.map_apply_delta(self.h, m, lane, d_in, stream or None), "map apply delta")
 
     def footprint(self) -> np.ndarray:
         nw = C.c_uint32()

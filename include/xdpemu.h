@@ -231,10 +231,15 @@ int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc
  * Values region of a map as a flat little-endian byte image (ARRAY: ValueSize*MaxEntries; HASH: the
  * device slot table's values, identical layout on every replica built the same way). */
 int xe_map_values_bytes(xe_vm* vm, int32_t map_idx, uint64_t* bytes);
-/* d_out (device, bytes) := current values - snapshot taken at the start of the last run (u64 words) */
-int xe_map_delta(xe_vm* vm, int32_t map_idx, void* d_out, void* stream);
-/* values := snapshot + d_in (u64 words, wrapping) */
-int xe_map_apply_delta(xe_vm* vm, int32_t map_idx, const void* d_in, void* stream);
+/* d_out (device, bytes) := current values - snapshot taken at the start of the last run, computed in
+ * lanes of `lane` bytes (1, 2, 4, 8; 0 = the map's own xe_map_delta_lane): a narrow counter wraps at
+ * its own width, so the cross-device sum must be taken in lanes of that width too */
+int xe_map_delta(xe_vm* vm, int32_t map_idx, uint32_t lane, void* d_out, void* stream);
+/* values := snapshot + d_in, in lanes of `lane` bytes (wrapping) */
+int xe_map_apply_delta(xe_vm* vm, int32_t map_idx, uint32_t lane, const void* d_in, void* stream);
+/* width in bytes of the last run's adds into this map (1, 2, 4 or 8), 0 when there were none; more
+ * than one width is an order-dependent run (replayed in order) and reports 8 */
+int xe_map_delta_lane(xe_vm* vm, int32_t map_idx, uint32_t* lane_bytes);
 /* footprint masks of the last run, for cross-shard conflict checks: 2 u64 per map (read, atomic) + flags */
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords);
 

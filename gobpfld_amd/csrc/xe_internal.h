@@ -93,8 +93,9 @@ struct XeDevMap {
   uint32_t max_entries;
   uint64_t vals_bytes;  // ARRAY: value_size*max_entries; HASH: (cap+1)*value_size
   uint8_t* vals;        // ARRAY memory / HASH slot values (slot cap = the nil-key slot)
-  uint64_t* keys;       // HASH: (cap+1) * kwords u64 words, zero padded
-  uint32_t* state;      // HASH: (cap+1) slot states
+  uint64_t* keys;       // HASH: (cap+1) slot records of rwords u64 words: [0] = slot state, then the
+                        // zero-padded key words (one probe touches one record, one cache line)
+  uint32_t* state;      // unused on the device (host-side layout keeps separate arrays)
   uint32_t* count;      // HASH: number of entries (device word)
   uint32_t cap;         // HASH: power-of-two slot count
   uint32_t kwords;      // HASH: (key_size+7)/8
@@ -103,8 +104,14 @@ struct XeDevMap {
   uint8_t* rep;
   uint64_t rep_stride;  // bytes between replicas
   uint32_t nrep;        // 1 = adds go to vals directly
-  uint32_t pad_;
+  uint32_t rwords;      // HASH: u64 words per slot record (power of two >= 1 + kwords)
 };
+
+XE_HD uint32_t xe_hash_rwords(uint32_t kwords) {
+  uint32_t r = 1;
+  while (r < 1 + kwords) r <<= 1;
+  return r;
+}
 
 // Word-wise multiplicative hash over the zero-padded key words. The reference hashes with sha256
 // (maps_hash.go:55); the function is unobservable (only key equality matters), so a cheap one is

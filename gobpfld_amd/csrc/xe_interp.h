@@ -446,7 +446,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   }
   uint32_t slot = xe_h_slot(h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
-  B.len = (((XE_GP(const uint32_t))M.state)[slot] & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
+  B.len = (uint32_t(((XE_GP(const uint64_t))M.keys)[uint64_t(slot) * M.rwords]) & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
   B.array = false;
   return true;
 }
@@ -823,20 +823,32 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
 }
 
 // ------------------------------------------------------------------ hash map
+XE_DEV uint32_t hash_state(const XeDevMap& M, uint64_t slot) {
+  return uint32_t(((XE_GP(const uint64_t))M.keys)[slot * M.rwords]);
+}
+XE_DEV void hash_set_state(const XeDevMap& M, uint64_t slot, uint32_t st) {
+  ((XE_GP(uint64_t))M.keys)[slot * M.rwords] = st;
+}
+
+// Linear probing over slot records: the state word and the key words of a record are loaded
+// together (independent loads of one line), then compared.
 XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
-  XE_GP(const uint32_t) state = (XE_GP(const uint32_t))M.state;
-  if (empty) return (state[M.cap] & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
+  if (empty) return (hash_state(M, M.cap) & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
   uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(hv) & mask;
 #pragma unroll 1
   for (uint32_t probe = 0; probe < M.cap; probe++) {
-    uint32_t st = state[idx];
-    if (!(st & XE_SLOT_FULL)) return -1;
-    XE_GP(const uint64_t) k = (XE_GP(const uint64_t))M.keys + uint64_t(idx) * M.kwords;
+    XE_GP(const uint64_t) r = (XE_GP(const uint64_t))M.keys + uint64_t(idx) * M.rwords;
+    uint64_t w[XE_MAX_KEY / 8 + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= XE_MAX_KEY / 8; k++)
+      if (k <= M.kwords) w[k] = r[k];
+    if (!(uint32_t(w[0]) & XE_SLOT_FULL)) return -1;
     bool eq = true;
-#pragma unroll 1
-    for (uint32_t w = 0; w < M.kwords; w++) eq = eq && (k[w] == kw[w]);
+#pragma unroll
+    for (uint32_t k = 0; k < XE_MAX_KEY / 8; k++)
+      if (k < M.kwords) eq = eq && (w[k + 1] == kw[k]);
     if (eq) return int64_t(idx);
     idx = (idx + 1) & mask;
   }
@@ -846,17 +858,17 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
 // insert a new key (sequential mode only); returns slot
 XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty) {
   if (empty) {
-    M.state[M.cap] = XE_SLOT_FULL;
+    hash_set_state(M, M.cap, XE_SLOT_FULL);
     *M.count += 1;
     return int64_t(M.cap);
   }
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
   uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(hv) & mask;
-  while (M.state[idx] & XE_SLOT_FULL) idx = (idx + 1) & mask;
-  uint64_t* k = M.keys + uint64_t(idx) * M.kwords;
+  while (hash_state(M, idx) & XE_SLOT_FULL) idx = (idx + 1) & mask;
+  uint64_t* k = M.keys + uint64_t(idx) * M.rwords + 1;
   for (uint32_t w = 0; w < M.kwords; w++) k[w] = kw[w];
-  M.state[idx] = XE_SLOT_FULL;
+  hash_set_state(M, idx, XE_SLOT_FULL);
   *M.count += 1;
   return int64_t(idx);
 }
@@ -974,9 +986,9 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     if (slot < 0) slot = hash_insert_new(M, kw, empty);
     uint8_t* dst = M.vals + uint64_t(slot) * M.value_size;
     if (ve) {
-      M.state[slot] |= XE_SLOT_VLEN0;  // nil backing
+      hash_set_state(M, uint64_t(slot), hash_state(M, uint64_t(slot)) | XE_SLOT_VLEN0);  // nil backing
     } else {
-      M.state[slot] &= ~XE_SLOT_VLEN0;
+      hash_set_state(M, uint64_t(slot), hash_state(M, uint64_t(slot)) & ~XE_SLOT_VLEN0);
       ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; }, cm3);
     }
     return helper_errno_result(L, 0);

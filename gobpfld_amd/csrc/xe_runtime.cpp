@@ -444,8 +444,7 @@ int map_alloc_device(HostMap& m) {
   m.rep_stride = (m.vals_alloc + 255) & ~uint64_t(255);
   if (m.nrep > 1 && dev_alloc((void**)&m.d_rep, m.rep_stride * m.nrep)) return -1;
   if (m.dkind == XE_DM_HASH) {
-    if (dev_alloc((void**)&m.d_keys, std::max<size_t>(size_t(m.cap + 1) * m.kwords * 8, 8))) return -1;
-    if (dev_alloc((void**)&m.d_state, size_t(m.cap + 1) * 4)) return -1;
+    if (dev_alloc((void**)&m.d_keys, size_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8)) return -1;
     if (dev_alloc((void**)&m.d_count, 8)) return -1;
   }
   return 0;
@@ -459,8 +458,15 @@ void map_free_device(HostMap& m) {
 int map_upload(xe_vm* vm, HostMap& m) {
   if (h2d(m.d_vals, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
   if (m.dkind == XE_DM_HASH) {
-    if (m.kwords && h2d(m.d_keys, m.keys.data(), size_t(m.cap + 1) * m.kwords * 8, vm->stream)) return -1;
-    if (h2d(m.d_state, m.state.data(), size_t(m.cap + 1) * 4, vm->stream)) return -1;
+    // interleave state and key words into the device slot records
+    const uint32_t rw = xe_hash_rwords(m.kwords);
+    std::vector<uint64_t> rec(size_t(m.cap + 1) * rw, 0);
+    for (size_t i = 0; i <= m.cap; i++) {
+      rec[i * rw] = m.state[i];
+      for (uint32_t w = 0; w < m.kwords; w++) rec[i * rw + 1 + w] = m.keys[i * m.kwords + w];
+    }
+    if (h2d(m.d_keys, rec.data(), rec.size() * 8, vm->stream)) return -1;
+    if (dsync(vm->stream)) return -1;  // rec is a host temporary
     if (h2d(m.d_count, &m.count, 4, vm->stream)) return -1;
   }
   if (dsync(vm->stream)) return -1;
@@ -472,8 +478,13 @@ int map_download(xe_vm* vm, HostMap& m) {
   if (!m.dev_dirty) return 0;
   if (d2h(m.vals.data(), m.d_vals, m.vals_alloc, vm->stream)) return -1;
   if (m.dkind == XE_DM_HASH) {
-    if (m.kwords && d2h(m.keys.data(), m.d_keys, size_t(m.cap + 1) * m.kwords * 8, vm->stream)) return -1;
-    if (d2h(m.state.data(), m.d_state, size_t(m.cap + 1) * 4, vm->stream)) return -1;
+    const uint32_t rw = xe_hash_rwords(m.kwords);
+    std::vector<uint64_t> rec(size_t(m.cap + 1) * rw, 0);
+    if (d2h(rec.data(), m.d_keys, rec.size() * 8, vm->stream) || dsync(vm->stream)) return -1;
+    for (size_t i = 0; i <= m.cap; i++) {
+      m.state[i] = uint32_t(rec[i * rw]);
+      for (uint32_t w = 0; w < m.kwords; w++) m.keys[i * m.kwords + w] = rec[i * rw + 1 + w];
+    }
     if (d2h(&m.count, m.d_count, 4, vm->stream)) return -1;
   }
   if (dsync(vm->stream)) return -1;
@@ -521,6 +532,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     d.count = m.d_count;
     d.cap = m.cap;
     d.kwords = m.kwords;
+    d.rwords = m.dkind == XE_DM_HASH ? xe_hash_rwords(m.kwords) : 0;
     d.rep = m.d_rep;
     d.rep_stride = m.rep_stride;
     d.nrep = m.nrep;

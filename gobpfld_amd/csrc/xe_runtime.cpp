@@ -432,18 +432,23 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 
 // Replicas of the value region for deferred 8-byte adds (XeDevMap::rep): enough to spread a hot
 // counter's atomics, bounded in memory (HBM is plentiful, but every run folds all replicas).
-uint32_t choose_nrep(uint64_t vals_alloc) {
+// Replicas of a value region spread contended map adds over nrep copies (wave % nrep), folded into
+// the region after the run. Chosen per run from the live bytes (ARRAY: the region; HASH: entries x
+// value size), bounded so the fold reads at most 128 MB. Measured: C3 (64K Zipf-hot flows in a
+// 1M-entry table) needs >= 4 (1 replica: 8.2 ms, 2: 1.1-4.0 ms depending on placement, 4: 1.08 ms);
+// C5 (1M uniform flows) is fastest with none (3.45 ms; each doubling costs ~5 %).
+uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc) {
   if (const char* e = getenv("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));  // tuning experiments
-  // measured: C3 (hot Zipf flows) needs >= 2, C5 (uniform flows, 32 MB of values) loses 5 % per doubling
-  return vals_alloc <= (8ull << 20) ? 16u : vals_alloc <= (256ull << 20) ? 2u : 1u;
+  uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
+  while (want > 1 && uint64_t(want) * vals_alloc > (128ull << 20)) want >>= 1;
+  return want;
 }
 
 int map_alloc_device(HostMap& m) {
   if (dev_alloc((void**)&m.d_vals, m.vals_alloc)) return -1;
   if (dev_alloc((void**)&m.d_snap, m.vals_alloc)) return -1;
-  m.nrep = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(m.vals_alloc) : 1u;
+  m.nrep = 1;  // replicas are sized per run (set_replicas)
   m.rep_stride = (m.vals_alloc + 255) & ~uint64_t(255);
-  if (m.nrep > 1 && dev_alloc((void**)&m.d_rep, m.rep_stride * m.nrep)) return -1;
   if (m.dkind == XE_DM_HASH) {
     if (dev_alloc((void**)&m.d_keys, size_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8)) return -1;
     if (dev_alloc((void**)&m.d_count, 8)) return -1;
@@ -516,6 +521,18 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.host_dirty && map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.count) * m.def.value_size : m.vals_bytes;
+    const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc) : 1u;
+    if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
+      dev_free(m.d_rep);
+      m.d_rep = nullptr;
+      m.nrep = 1;
+      if (want > 1 && (dev_alloc((void**)&m.d_rep, m.rep_stride * want) ||
+                       dmemset(m.d_rep, 0, m.rep_stride * want, vm->stream) || dsync(vm->stream)))
+        return fail(vm, XE_ERR_DEVICE, "device alloc (map replicas)");
+      m.nrep = want;
+      vm->jit_idx = -1;  // the replica count is compiled into the per-program kernel
+    }
   }
   std::vector<XeDevMap> dm(vm->maps.size());
   memset(dm.data(), 0, dm.size() * sizeof(XeDevMap));
@@ -666,10 +683,6 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
   if (set_device(vm->settings.device) || map_alloc_device(m)) {
     map_free_device(m);
     return fail(vm, XE_ERR_DEVICE, "device alloc (map)");
-  }
-  if (m.d_rep && (dmemset(m.d_rep, 0, m.rep_stride * m.nrep, vm->stream) || dsync(vm->stream))) {
-    map_free_device(m);
-    return fail(vm, XE_ERR_DEVICE, "replica init");
   }
   m.host_dirty = true;
   vm->maps.push_back(std::move(m));

@@ -39,6 +39,11 @@ class Settings(C.Structure):  # emulator/vm.go:282-296 + device knobs
                 ("engine", C.c_uint32)]
 
 
+class PcapInfo(C.Structure):  # include/xdpemu_io.h
+    _fields_ = [("linktype", C.c_uint32), ("snaplen", C.c_uint32), ("nanosecond", C.c_uint32),
+                ("swapped", C.c_uint32), ("first_record", C.c_uint64)]
+
+
 class BatchStats(C.Structure):
     _fields_ = [("packets", C.c_uint64), ("steps", C.c_uint64), ("status_count", C.c_uint64 * 8),
                 ("mode_used", C.c_uint32), ("conflict", C.c_uint32), ("kernel_ms", C.c_float),
@@ -82,6 +87,13 @@ _SIGS = {
     "version": (C.c_char_p, []),
     "device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "decode_names": (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t]),
+    # include/xdpemu_io.h
+    "pcap_header": (C.c_int, [P, C.c_uint64, P]),
+    "pcap_count": (C.c_int, [P, C.c_uint64, P, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "pcap_fill": (C.c_int, [P, C.c_uint64, P, C.POINTER(C.c_uint64), P, C.c_uint64, C.c_uint32, C.c_uint32, P,
+                            C.c_uint64, C.c_uint32, P, P, P, C.POINTER(C.c_uint32)]),
+    "pcap_pack": (C.c_int, [P, C.c_uint64, P, C.POINTER(C.c_uint64), P, C.c_uint64, C.c_uint32, C.c_uint32,
+                            C.c_uint32, P, P, P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
 }
 
 # every symbol include/xdpemu.h declares (checked by tests/test_abi.py)
@@ -92,6 +104,7 @@ HEADER_SYMBOLS = [
     "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
     "xe_device_count",
 ]
+IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h
 
 
 class Lib:

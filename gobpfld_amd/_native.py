@@ -137,5 +137,9 @@ def product() -> Lib:
     global _product
     if _product is None:
         import os
+        try:  # torch bundles its own HIP runtime: have it loaded first so the process holds one
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _product = Lib(os.environ.get("XE_LIB", PRODUCT_LIB), "xe_")
     return _product

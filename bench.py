@@ -50,8 +50,11 @@ def pmc_traffic(name: str, n: int) -> tuple[float | None, str | None]:
     """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE x2 per
     the gfx950 correction + WRITE_SIZE; profiles/r1/<config>_traffic.json, made by
     scripts/pmc_traffic.py), when one exists for this exact batch size; else (None, None)."""
-    f = ROOT / "profiles" / "r1" / f"{name}_traffic.json"
-    if not f.exists():
+    for rnd in ("r2", "r1"):  # newest committed PMC passes first
+        f = ROOT / "profiles" / rnd / f"{name}_traffic.json"
+        if f.exists():
+            break
+    else:
         return None, None
     d = json.loads(f.read_text())
     if d.get("workload") != name or int(d.get("packets", -1)) != n:
@@ -85,6 +88,29 @@ def _oracle_rate(name: str, start: int, n: int) -> tuple[float, float]:
     return time.perf_counter() - t0, ipp
 
 
+def host_cpu_info() -> dict:
+    """The host the CPU baseline runs on: `nproc` (all CPUs of the machine), the CPUs this process may
+    run on (sched_getaffinity), the per-job CPU share the GPU pool grants (OMP_NUM_THREADS on the box,
+    16 per GPU; a pool of more threads than the share only oversubscribes it) and the lscpu model."""
+    ncpu = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = ncpu
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, share) if share > 0 else aff
+    return {"nproc": ncpu, "affinity_cpus": aff, "job_cpu_share": share or None, "usable_cpus": max(1, usable),
+            "cpu_model": model}
+
+
 def cpu_baseline(name: str, n_sample: int, target_s: float = 12.0, threads: int = 0) -> dict:
     """The oracle (C++ restatement of emulator/) timed on a bounded prefix of the workload: one thread,
     then `threads` threads, each a private VM over a contiguous shard (valid: the configs' map
@@ -94,7 +120,8 @@ def cpu_baseline(name: str, n_sample: int, target_s: float = 12.0, threads: int 
     from concurrent.futures import ThreadPoolExecutor
     from gobpfld_amd import build as B
     B.build_oracle()
-    threads = threads or min(16, os.cpu_count() or 1)
+    host = host_cpu_info()
+    threads = threads or host["usable_cpus"]
     cal_dt, _ = _oracle_rate(name, 0, 20_000)
     r1 = 20_000 / cal_dt
     n1 = n_sample or int(min(max(r1 * target_s / 2, 50_000), 8_000_000))
@@ -107,6 +134,7 @@ def cpu_baseline(name: str, n_sample: int, target_s: float = 12.0, threads: int 
         list(ex.map(_oracle_run, jobs))
         dtt = time.perf_counter() - t0
     return {"value": round(per * threads / dtt / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+            "host": host,
             "single_thread_value": round(n1 / dt1 / 1e6, 4),
             "sample": f"{per * threads} packets of {name} on {threads} threads (private VMs on contiguous shards, "
                       f"{dtt:.2f} s wall) and the first {n1} packets on 1 thread ({dt1:.2f} s) through "
@@ -136,6 +164,62 @@ def e2e_baseline(vm, umem: np.ndarray, descs: np.ndarray, iters: int = 3) -> dic
             "path": "pinned host UMEM + descriptors -> H2D -> kernel -> D2H verdicts (xe_run_batch_host)"}
 
 
+def single_process_multi(args, name: str, n: int) -> None:
+    """`bench.py --gpus N` without torchrun: one process drives N GPUs through the C ABI
+    (xe_multi_create / xe_run_batch_multi: concurrent shards, RCCL delta all-reduce or in-order
+    replay), the path a Go host uses through the FFI alone. Same JSON line as the torchrun form."""
+    import torch
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import Multi, VM, Settings
+    G = args.gpus
+    engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
+    vms, bufs, sizes = [], [], None
+    for k in range(G):
+        dev = torch.device("cuda", k)
+        umem, descs = W.build_batch(name, k * n, n)
+        if k == 0:
+            sizes = descs["len"].astype(np.int64)
+        bufs.append((torch.from_numpy(umem).to(dev), torch.from_numpy(descs.view(np.uint8)).to(dev),
+                     torch.zeros(n, dtype=torch.int32, device=dev)))
+        vm = VM(Settings(device=k, engine=engine))
+        W.setup_vm(vm, name)
+        vms.append(vm)
+    mu = Multi(vms)
+    args_run = ([u.data_ptr() for u, _, _ in bufs], [u.numel() for u, _, _ in bufs], [d.data_ptr() for _, d, _ in bufs],
+                [n] * G)
+    for _ in range(args.warmup):
+        mu.run(*args_run, d_verdicts=[v.data_ptr() for _, _, v in bufs])
+    for k in range(G):
+        torch.cuda.synchronize(k)
+    kernel_ms, replays, steps_retired = [], 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sts, rep = mu.run(*args_run, d_verdicts=[v.data_ptr() for _, _, v in bufs])
+        kernel_ms.append(sts[0]["kernel_ms"])
+        steps_retired += sts[0]["steps"]
+        replays += int(rep)
+    for k in range(G):
+        torch.cuda.synchronize(k)
+    elapsed = time.perf_counter() - t0
+    value = n * G * args.steps / elapsed / 1e6
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    achieved = float(alg_bytes_per_packet(name, sizes).sum()) / avg_kernel_s / 1e9
+    print(json.dumps({
+        "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches", "value": round(value, 3),
+        "unit": "Mpkt/s", "n_gpus": G, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic splitmix64 packets, SURVEY §8d)",
+        "config": {"workload": WORKLOADS[name], "packets_per_gpu": n, "parallelism": f"dp{G} (one process, xe_run_batch_multi)",
+                   "insns_per_packet": round(steps_retired / max(1, n * args.steps), 2), "in_order_replays": replays},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                     "kernel": "device 0 emulator kernel"},
+        "cpu_baseline": None}), flush=True)
+    mu.close()
+    for v in vms:
+        v.close()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,6 +237,10 @@ def main() -> None:
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1:
+        from gobpfld_amd import workloads as W
+        n1 = args.packets or (W.CONFIGS[args.config]["n"] // (8 if args.config == "c5" else 1))
+        return single_process_multi(args, args.config, n1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -162,7 +250,7 @@ def main() -> None:
 
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
-    from gobpfld_amd.shard import allreduce_map_deltas
+    from gobpfld_amd.shard import exchange_shards
 
     name = args.config
     n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))
@@ -181,14 +269,18 @@ def main() -> None:
     vm = VM(Settings(device=local, engine=engine))
     W.setup_vm(vm, name)
     maps = list(vm.map_defs)
-    deltas = {m: torch.zeros(vm.map_values_bytes(m), dtype=torch.uint8, device=dev) for m in maps}
     stream = torch.cuda.current_stream(dev).cuda_stream
+    exchanges = {"exact_sum": 0, "replayed": 0}
+
+    def run() -> dict:
+        return vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
+                                   d_verdicts=d_ver.data_ptr(), stream=stream)
 
     def step() -> dict:
-        st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
-                                 d_verdicts=d_ver.data_ptr(), stream=stream)
-        if world > 1:  # map-value deltas -> one RCCL all-reduce per map -> every replica
-            allreduce_map_deltas(vm, maps, deltas, dist, stream=stream)
+        st = run()
+        if world > 1:  # footprint check, then one RCCL all-reduce per map (or the in-order replay)
+            x = exchange_shards(vm, maps, dist, run, device=dev, stream=stream)
+            exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
         return st
 
     for _ in range(args.warmup):
@@ -253,11 +345,13 @@ def main() -> None:
                        "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
                        "engine": sorted(engines),
                        "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps),
+                       "shard_exchanges": exchanges if world > 1 else None,
                        "grid": grid},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
                          "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                          "kernel": "xe_jit_kernel" if engines == {"jit"} else "xe_interp_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel_ms_steps": [round(k, 4) for k in kernel_ms],
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "alg_bytes_per_packet": ALG_DESC.get(name, "16 desc + min(len,64) header + 4 verdict"),
                          "issue_frac": round(insns_per_pkt * n / avg_kernel_s / ISSUE_PEAK, 5)},

@@ -5,6 +5,9 @@
  *
  * The program counts packets per EtherType low byte in an ARRAY map and returns XDP_PASS:
  *   r2 = *(u8 *)(ctx->data + 13); key = r2; v = lookup(map 1, &key); if v: *v += 1 (lock xadd)
+ * The map starts from initial data given the way gobpfld's AbstractMap.InitialData holds it
+ * ({int key: []byte value}, map_abstract.go:33), flattened as ArrayMap.Init does
+ * (emulator/maps_array.go:19-44) — the same translation as INTEGRATION.md's initialImage.
  *
  *   gcc -O2 -Iinclude examples/xdp_batch.c -Lgobpfld_amd -lxdpemu -Wl,-rpath,$PWD/gobpfld_amd
  */
@@ -17,6 +20,29 @@
 /* eBPF instruction: op, dst | src << 4, off, imm (little endian, ebpf/ebpf.go:46-76) */
 static uint64_t insn(uint8_t op, uint8_t dst, uint8_t src, int16_t off, int32_t imm) {
   return (uint64_t)op | (uint64_t)(dst | (src << 4)) << 8 | (uint64_t)(uint16_t)off << 16 | (uint64_t)(uint32_t)imm << 32;
+}
+
+/* one InitialData entry: key -> value bytes */
+typedef struct { int key; const uint8_t* val; size_t len; } initial_entry;
+
+/* ArrayMap.Init: copy each value at key*ValueSize (running on into later entries when longer) in
+ * ascending key order (Go ranges over the map in random order; order only matters when copies
+ * overlap); a key past the memory is an error (Go panics on the slice bound). */
+static int initial_image(const xe_map_def* d, const initial_entry* e, size_t n, uint8_t* img) {
+  const size_t size = (size_t)d->value_size * d->max_entries;
+  memset(img, 0, size);
+  int last = -1;
+  for (size_t done = 0; done < n; done++) {
+    const initial_entry* next = NULL;  /* smallest key above the last one applied */
+    for (size_t j = 0; j < n; j++)
+      if (e[j].key > last && (!next || e[j].key < next->key)) next = &e[j];
+    if (!next) break;
+    if (next->key < 0 || (size_t)next->key * d->value_size > size) return -1;
+    const size_t off = (size_t)next->key * d->value_size;
+    memcpy(img + off, next->val, next->len < size - off ? next->len : size - off);
+    last = next->key;
+  }
+  return 0;
 }
 
 int main(int argc, char** argv) {
@@ -40,10 +66,15 @@ int main(int argc, char** argv) {
   xe_vm* vm = NULL;
   int32_t map = 0, p = 0;
   xe_map_def def = {XE_MAP_ARRAY, 4, 8, 256, 0};
+  /* InitialData {2: u64 7, 0: u64 1000} */
+  static const uint8_t v0[8] = {0xe8, 0x03}, v2[8] = {7};
+  const initial_entry init[] = {{2, v2, 8}, {0, v0, 8}};
+  uint8_t img[256 * 8];
   xe_default_settings(&s);
   int rc = xe_create(&s, &vm);
   if (rc) { printf("xe_create: %d\n", rc); return 2; }
-  if ((rc = xe_add_map(vm, &def, NULL, 0, &map)) || (rc = xe_add_raw_program(vm, prog, sizeof prog / 8, &p)) ||
+  if (initial_image(&def, init, 2, img)) { printf("initial data outside the map\n"); return 1; }
+  if ((rc = xe_add_map(vm, &def, img, sizeof img, &map)) || (rc = xe_add_raw_program(vm, prog, sizeof prog / 8, &p)) ||
       (rc = xe_set_entrypoint(vm, p))) {
     printf("setup: %d %s\n", rc, xe_last_error(vm));
     return 1;
@@ -71,5 +102,5 @@ int main(int argc, char** argv) {
   free(umem);
   free(desc);
   free(verdicts);
-  return pass == n && counts[0] + counts[1] + counts[2] == n ? 0 : 1;
+  return pass == n && counts[0] + counts[1] + counts[2] == (uint64_t)n + 1007 && counts[0] >= 1000 && counts[2] >= 7 ? 0 : 1;
 }

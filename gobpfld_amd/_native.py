@@ -84,6 +84,14 @@ _SIGS = {
     "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
     "map_delta_lane": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint32)]),
     "footprint": (C.c_int, [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "shard_check": (C.c_int, [P, C.c_uint32, C.c_uint32, P]),
+    "map_state_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
+    "map_state_export": (C.c_int, [P, C.c_int32, P, P]),
+    "map_state_import": (C.c_int, [P, C.c_int32, P, P]),
+    "multi_create": (C.c_int, [P, C.c_uint32, C.POINTER(P)]),
+    "multi_destroy": (None, [P]),
+    "multi_last_error": (C.c_char_p, [P]),
+    "run_batch_multi": (C.c_int, [P, P, P, P, P, P, P, P, P]),
     "version": (C.c_char_p, []),
     "device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "decode_names": (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t]),
@@ -102,7 +110,8 @@ HEADER_SYMBOLS = [
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
     "xe_map_count", "xe_map_dump", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
     "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
-    "xe_device_count",
+    "xe_device_count", "xe_shard_check", "xe_map_state_bytes", "xe_map_state_export", "xe_map_state_import",
+    "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h
 

@@ -139,6 +139,7 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 // flags word bits (device -> host)
 #define XE_FLAG_ORDERED 1u   // a lane needed a non-commutative map write in parallel mode
 #define XE_FLAG_CAPACITY 2u
+#define XE_FLAG_UNALIGNED 4u  // a map add not aligned to its own width (cross-shard delta lanes inexact)
 
 // per-launch parameters
 struct XeParams {

@@ -408,8 +408,9 @@ XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
 
 // atomic adds of different widths on one map do not commute in general (a narrow add stops its
 // carry at its own top byte): the host treats a map with more than one width class as a conflict
-XE_DEV void width_record(XeLane& L, uint32_t m, int size) {
+XE_DEV void width_record(XeLane& L, const XeParams& P, uint32_t m, int size, uint64_t addr) {
   const uint32_t cls = size == 8 ? 3u : size == 4 ? 2u : size == 2 ? 1u : 0u;
+  if (addr & uint64_t(size - 1)) xe_atomic_or32(P.flags, XE_FLAG_UNALIGNED);
   if (m >= 1 && m <= 4) L.awidth |= 1u << (4 * m + cls);
   else xe_atomic_or64(&L.rep[XE_REC_WIDTH0 + m / 16], 1ull << (4 * (m % 16) + cls));
 }
@@ -1231,7 +1232,7 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
   fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
-  width_record(L, B.map, size);
+  width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
   wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
   return 0;
 }

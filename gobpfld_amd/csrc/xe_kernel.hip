@@ -30,15 +30,23 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
 
 // Map-value deltas for the multi-GPU reduction, lane-wise at the width of the map's adds (T): a
 // narrow counter wraps at its own width, so a u64 word difference would borrow across fields.
-template <class T>
-__global__ void xe_delta_kernel(const T* cur, const T* snap, T* out, uint64_t n) {
+// C is the reduction container: T itself, except u16 lanes which travel as u32 (RCCL has no 16-bit
+// integer sum); the container sum is truncated back to T on apply, so it wraps exactly like T.
+template <class T, class C>
+__global__ void xe_delta_kernel(const T* cur, const T* snap, C* out, uint64_t n) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
-    out[i] = T(cur[i] - snap[i]);
+    out[i] = C(T(cur[i] - snap[i]));
 }
-template <class T>
-__global__ void xe_apply_delta_kernel(T* cur, const T* snap, const T* delta, uint64_t n) {
+template <class T, class C>
+__global__ void xe_apply_delta_kernel(T* cur, const T* snap, const C* delta, uint64_t n) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
-    cur[i] = T(snap[i] + delta[i]);
+    cur[i] = T(snap[i] + T(delta[i]));
+}
+// acc[i] += in[i] over containers (VMs sharing one device exchange through this instead of RCCL)
+template <class C>
+__global__ void xe_sum_kernel(C* acc, const C* in, uint64_t n) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    acc[i] = C(acc[i] + in[i]);
 }
 
 // vals += sum of the replicas; replicas := 0 (only words that received adds are written). All nrep
@@ -88,25 +96,40 @@ extern "C" int xe_interp_occupancy(uint32_t nmaps) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, xe_interp_kernel, 256, (nmaps + 1) * sizeof(XeDevMap)) != hipSuccess) return 0;
   return nb;
 }
-template <class T>
+template <class T, class C = T>
 static int launch_delta_t(const void* cur, const void* snap, void* out, uint64_t n, hipStream_t s) {
   uint32_t blocks = uint32_t(n / 256 + 1);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(xe_delta_kernel<T>, dim3(blocks), dim3(256), 0, s, (const T*)cur, (const T*)snap, (T*)out, n);
+  hipLaunchKernelGGL((xe_delta_kernel<T, C>), dim3(blocks), dim3(256), 0, s, (const T*)cur, (const T*)snap, (C*)out, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-template <class T>
+template <class T, class C = T>
 static int launch_apply_t(void* cur, const void* snap, const void* delta, uint64_t n, hipStream_t s) {
   uint32_t blocks = uint32_t(n / 256 + 1);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(xe_apply_delta_kernel<T>, dim3(blocks), dim3(256), 0, s, (T*)cur, (const T*)snap, (const T*)delta, n);
+  hipLaunchKernelGGL((xe_apply_delta_kernel<T, C>), dim3(blocks), dim3(256), 0, s, (T*)cur, (const T*)snap, (const C*)delta, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template <class C>
+static int launch_sum_t(void* acc, const void* in, uint64_t n, hipStream_t s) {
+  uint32_t blocks = uint32_t(n / 256 + 1);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL((xe_sum_kernel<C>), dim3(blocks), dim3(256), 0, s, (C*)acc, (const C*)in, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// acc += in over the delta containers of `lane` for a value region of `bytes`
+extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s) {
+  switch (lane) {
+    case 1: return launch_sum_t<uint8_t>(acc, in, bytes, s);
+    case 2: case 4: return launch_sum_t<uint32_t>(acc, in, bytes / lane, s);
+    default: return launch_sum_t<unsigned long long>(acc, in, bytes / 8, s);
+  }
 }
 // bytes: length of the value region (multiple of 8); lane: 1, 2, 4 or 8
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, hipStream_t s) {
   switch (lane) {
     case 1: return launch_delta_t<uint8_t>(cur, snap, out, bytes, s);
-    case 2: return launch_delta_t<uint16_t>(cur, snap, out, bytes / 2, s);
+    case 2: return launch_delta_t<uint16_t, uint32_t>(cur, snap, out, bytes / 2, s);
     case 4: return launch_delta_t<uint32_t>(cur, snap, out, bytes / 4, s);
     default: return launch_delta_t<unsigned long long>(cur, snap, out, bytes / 8, s);
   }
@@ -115,7 +138,7 @@ extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* de
                                      hipStream_t s) {
   switch (lane) {
     case 1: return launch_apply_t<uint8_t>(cur, snap, delta, bytes, s);
-    case 2: return launch_apply_t<uint16_t>(cur, snap, delta, bytes / 2, s);
+    case 2: return launch_apply_t<uint16_t, uint32_t>(cur, snap, delta, bytes / 2, s);
     case 4: return launch_apply_t<uint32_t>(cur, snap, delta, bytes / 4, s);
     default: return launch_apply_t<unsigned long long>(cur, snap, delta, bytes / 8, s);
   }

@@ -30,6 +30,7 @@ extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uin
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane,
                                      hipStream_t s);
 extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
@@ -54,7 +55,7 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeMem M;
   XeLane L;
   L.mem = &M;
-  static uint8_t hdrbuf[XE_HDR_WAVE_BYTES];
+  static thread_local uint8_t hdrbuf[XE_HDR_WAVE_BYTES];  // one per host thread (xe_multi runs shards concurrently)
   L.hdrbuf = hdrbuf;
   XePend pend;
   stage_maps(L, *P, nullptr);
@@ -68,18 +69,22 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   return 0;
 }
 int launch_jit(void*, const XeParams* P, uint32_t b, uint32_t t, xe_stream_t s) { return launch_interp(P, b, t, s); }
-template <class T>
+template <class T, class C = T>
 void lanes_sub(const void* a, const void* b, void* o, uint64_t n) {
-  for (uint64_t i = 0; i < n; i++) ((T*)o)[i] = T(((const T*)a)[i] - ((const T*)b)[i]);
+  for (uint64_t i = 0; i < n; i++) ((C*)o)[i] = C(T(((const T*)a)[i] - ((const T*)b)[i]));
 }
-template <class T>
-void lanes_add(const void* a, const void* b, void* o, uint64_t n) {
-  for (uint64_t i = 0; i < n; i++) ((T*)o)[i] = T(((const T*)a)[i] + ((const T*)b)[i]);
+template <class T, class C = T>
+void lanes_add(const void* snap, const void* d, void* o, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) ((T*)o)[i] = T(((const T*)snap)[i] + T(((const C*)d)[i]));
+}
+template <class C>
+void lanes_acc(void* acc, const void* in, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) ((C*)acc)[i] = C(((C*)acc)[i] + ((const C*)in)[i]);
 }
 int launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, xe_stream_t) {
   switch (lane) {
     case 1: lanes_sub<uint8_t>(cur, snap, out, bytes); break;
-    case 2: lanes_sub<uint16_t>(cur, snap, out, bytes / 2); break;
+    case 2: lanes_sub<uint16_t, uint32_t>(cur, snap, out, bytes / 2); break;
     case 4: lanes_sub<uint32_t>(cur, snap, out, bytes / 4); break;
     default: lanes_sub<uint64_t>(cur, snap, out, bytes / 8); break;
   }
@@ -88,9 +93,17 @@ int launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, u
 int launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane, xe_stream_t) {
   switch (lane) {
     case 1: lanes_add<uint8_t>(snap, delta, cur, bytes); break;
-    case 2: lanes_add<uint16_t>(snap, delta, cur, bytes / 2); break;
+    case 2: lanes_add<uint16_t, uint32_t>(snap, delta, cur, bytes / 2); break;
     case 4: lanes_add<uint32_t>(snap, delta, cur, bytes / 4); break;
     default: lanes_add<uint64_t>(snap, delta, cur, bytes / 8); break;
+  }
+  return 0;
+}
+int launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, xe_stream_t) {
+  switch (lane) {
+    case 1: lanes_acc<uint8_t>(acc, in, bytes); break;
+    case 2: case 4: lanes_acc<uint32_t>(acc, in, bytes / lane); break;
+    default: lanes_acc<uint64_t>(acc, in, bytes / 8); break;
   }
   return 0;
 }
@@ -134,6 +147,9 @@ int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t b, uint3
   return xe_launch_apply_delta(c, sn, d, b, lane, s);
 }
 int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t s) { return xe_launch_rep_fold(v, r, sw, nrep, nw, s); }
+int launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, xe_stream_t s) {
+  return xe_launch_delta_sum(acc, in, bytes, lane, s);
+}
 int launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg, void* zero, uint64_t zw,
                     xe_stream_t s) {
   return xe_launch_prologue(src, dst, words, nseg, zero, zw, s);
@@ -319,7 +335,9 @@ struct HostMap {
   uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
   uint32_t nrep = 1;
   uint64_t rep_stride = 0;
-  uint32_t lane = 0;  // width of the map adds of the last run (delta lanes): 0 none, 8 when mixed
+  uint32_t lane = 0;    // width of the map adds of the last run (delta lanes): 0 none, 8 when mixed
+  uint32_t wclass = 0;  // width classes of the last run's adds (bit 0: 1 B ... bit 3: 8 B)
+  uint32_t live = 0;    // HASH: entry count for replica sizing (host count, refreshed after ordered runs)
   bool host_dirty = true, dev_dirty = false;
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -400,6 +418,7 @@ struct xe_vm {
   void* d_regs = nullptr; size_t d_regs_cap = 0;
   std::vector<unsigned long long> last_fp;
   uint32_t last_flags = 0;
+  uint32_t last_mode = 0;  // XE_MODE_PARALLEL / XE_MODE_SEQUENTIAL of the last run
   // per-program kernel (JIT engine) for the current entry program
   int32_t jit_idx = -1;
   size_t jit_nmaps = 0;
@@ -463,6 +482,8 @@ void map_free_device(HostMap& m) {
 
 int map_upload(xe_vm* vm, HostMap& m) {
   if (h2d(m.d_vals, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
+  // the delta base is the uploaded state until a run takes its own snapshot
+  if (h2d(m.d_snap, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
   if (m.dkind == XE_DM_HASH) {
     // interleave state and key words into the device slot records
     const uint32_t rw = xe_hash_rwords(m.kwords);
@@ -477,6 +498,7 @@ int map_upload(xe_vm* vm, HostMap& m) {
   }
   if (dsync(vm->stream)) return -1;
   m.host_dirty = false;
+  m.live = m.count;
   return 0;
 }
 
@@ -495,6 +517,7 @@ int map_download(xe_vm* vm, HostMap& m) {
   }
   if (dsync(vm->stream)) return -1;
   m.dev_dirty = false;
+  m.live = m.count;
   return 0;
 }
 
@@ -521,7 +544,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.host_dirty && map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
-    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.count) * m.def.value_size : m.vals_bytes;
+    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
     const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc) : 1u;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
       dev_free(m.d_rep);
@@ -1023,9 +1046,20 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   }
   for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
     const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
+    vm->maps[m].wclass = wc;
     vm->maps[m].lane = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
   }
+  if (used == XE_MODE_SEQUENTIAL) {
+    // in-program inserts change the entry count: refresh the replica-sizing hint
+    std::vector<uint32_t> counts(vm->maps.size(), 0);
+    for (size_t i = 1; i < vm->maps.size(); i++)
+      if (vm->maps[i].dkind == XE_DM_HASH && d2h(&counts[i], vm->maps[i].d_count, 4, s)) return fail(vm, XE_ERR_DEVICE, "count");
+    if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
+    for (size_t i = 1; i < vm->maps.size(); i++)
+      if (vm->maps[i].dkind == XE_DM_HASH) vm->maps[i].live = counts[i];
+  }
   vm->last_flags = uint32_t(red[0]);
+  vm->last_mode = used;
   vm->last_fp.assign(red.begin() + 16, red.end());
   for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   if (stats) {
@@ -1110,13 +1144,90 @@ int xe_map_delta_lane(xe_vm* vm, int32_t mi, uint32_t* lane_bytes) {
 
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords) {
   if (!vm) return XE_ERR_INVAL;
-  uint32_t nm = uint32_t(vm->maps.size());
-  uint32_t need = 1 + 2 * nm;
+  const uint32_t nm = uint32_t(vm->maps.size() - 1);
+  const uint32_t need = 1 + 3 * nm;
   if (nwords) *nwords = need;
   if (!out) return XE_OK;
   if (cap_words < need) return XE_ERR_INVAL;
-  out[0] = vm->last_flags;
-  for (uint32_t i = 0; i < 2 * nm; i++) out[1 + i] = i < vm->last_fp.size() ? vm->last_fp[i] : 0;
+  uint64_t f = 0;
+  if (vm->last_flags & XE_FLAG_ORDERED) f |= XE_FPF_ORDERED;
+  if (vm->last_mode == XE_MODE_SEQUENTIAL) f |= XE_FPF_SEQUENTIAL;
+  if (vm->last_flags & XE_FLAG_UNALIGNED) f |= XE_FPF_UNALIGNED;
+  out[0] = f;
+  for (uint32_t m = 1; m <= nm; m++) {
+    const size_t r = 2 * size_t(m);
+    out[1 + 3 * (m - 1)] = r < vm->last_fp.size() ? vm->last_fp[r] : 0;
+    out[2 + 3 * (m - 1)] = r + 1 < vm->last_fp.size() ? vm->last_fp[r + 1] : 0;
+    out[3 + 3 * (m - 1)] = vm->maps[m].wclass;
+  }
+  return XE_OK;
+}
+
+int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_t* lanes) {
+  if (!fps || !ngpus || nwords < 1 || (nwords - 1) % 3) return XE_ERR_INVAL;
+  const uint32_t nm = (nwords - 1) / 3;
+  bool ok = true;
+  for (uint32_t m = 0; m < nm; m++) {
+    uint64_t added = 0;  // fields earlier shards added to
+    uint32_t wc = 0;
+    for (uint32_t k = 0; k < ngpus; k++) {
+      const uint64_t* f = fps + size_t(k) * nwords;
+      if (f[1 + 3 * m] & added) ok = false;  // shard k read a field an earlier shard changed
+      added |= f[2 + 3 * m];
+      wc |= uint32_t(f[3 + 3 * m]);
+    }
+    if (wc & (wc - 1)) ok = false;  // two widths: a narrow add's carry stops at its own field
+    if (lanes) lanes[m] = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
+  }
+  for (uint32_t k = 0; k < ngpus; k++)
+    if (fps[size_t(k) * nwords] & (XE_FPF_ORDERED | XE_FPF_SEQUENTIAL | XE_FPF_UNALIGNED)) ok = false;
+  return ok ? 1 : 0;
+}
+
+int xe_map_state_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !bytes) return XE_ERR_INVAL;
+  *bytes = m->vals_alloc + (m->dkind == XE_DM_HASH ? uint64_t(m->cap + 1) * xe_hash_rwords(m->kwords) * 8 + 8 : 0);
+  return XE_OK;
+}
+
+// [values][slot records][count u32, pad]: device-to-device copies on the VM's device
+int xe_map_state_export(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !d_out) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (m->host_dirty && map_upload(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+  uint8_t* o = (uint8_t*)d_out;
+  if (d2d(o, m->d_vals, m->vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "state export");
+  if (m->dkind == XE_DM_HASH) {
+    const uint64_t rb = uint64_t(m->cap + 1) * xe_hash_rwords(m->kwords) * 8;
+    if (d2d(o + m->vals_alloc, m->d_keys, rb, s) || d2d(o + m->vals_alloc + rb, m->d_count, 4, s))
+      return fail(vm, XE_ERR_DEVICE, "state export");
+  }
+  if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "state export");
+  return XE_OK;
+}
+
+int xe_map_state_import(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !d_in) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (m->host_dirty && map_upload(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+  const uint8_t* in = (const uint8_t*)d_in;
+  if (d2d(m->d_vals, in, m->vals_alloc, s) || d2d(m->d_snap, in, m->vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "state import");
+  if (m->dkind == XE_DM_HASH) {
+    const uint64_t rb = uint64_t(m->cap + 1) * xe_hash_rwords(m->kwords) * 8;
+    if (d2d(m->d_keys, in + m->vals_alloc, rb, s) || d2d(m->d_count, in + m->vals_alloc + rb, 4, s))
+      return fail(vm, XE_ERR_DEVICE, "state import");
+    uint32_t c = 0;
+    if (d2h(&c, m->d_count, 4, s)) return fail(vm, XE_ERR_DEVICE, "state import");
+    if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "state import");
+    m->live = c;
+  }
+  if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "state import");
+  m->dev_dirty = true;
   return XE_OK;
 }
 
@@ -1137,6 +1248,31 @@ int xe_debug_may_write_packet(const uint64_t* insns, uint32_t n) {
   int rc = translate(insns, n, prog, err);
   if (rc) return rc;
   return may_write_packet(prog) ? 1 : 0;
+}
+
+// ---- internal hooks for xe_multi.cpp (not part of include/xdpemu.h)
+int xe_internal_vm_device(const xe_vm* vm) { return vm ? vm->settings.device : -1; }
+void* xe_internal_vm_stream(xe_vm* vm) { return vm ? (void*)vm->stream : nullptr; }
+int xe_internal_nmaps(const xe_vm* vm) { return vm ? int(vm->maps.size()) - 1 : -1; }
+int xe_internal_may_write_packet(const xe_vm* vm) {
+  if (!vm || vm->entry < 1 || vm->entry >= int32_t(vm->programs.size())) return 1;
+  return may_write_packet(vm->programs[vm->entry]) ? 1 : 0;
+}
+int xe_internal_delta_sum(xe_vm* vm, void* acc, const void* in, uint64_t bytes, uint32_t lane) {
+  set_device(vm->settings.device);
+  return launch_delta_sum(acc, in, bytes, lane, vm->stream) || dsync(vm->stream) ? XE_ERR_DEVICE : XE_OK;
+}
+int xe_internal_alloc(xe_vm* vm, void** p, uint64_t bytes) {
+  set_device(vm->settings.device);
+  return dev_alloc(p, size_t(bytes)) ? XE_ERR_NOMEM : XE_OK;
+}
+void xe_internal_free(xe_vm* vm, void* p) {
+  set_device(vm->settings.device);
+  dev_free(p);
+}
+int xe_internal_copy(xe_vm* vm, void* dst, const void* src, uint64_t bytes) {
+  set_device(vm->settings.device);
+  return d2d(dst, src, size_t(bytes), vm->stream) || dsync(vm->stream) ? XE_ERR_DEVICE : XE_OK;
 }
 
 const char* xe_version(void) {

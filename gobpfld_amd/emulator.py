@@ -59,6 +59,27 @@ class BatchResult:
     stats: dict
 
 
+def initial_image(d: MapDef, data: dict) -> bytes | None:
+    """AbstractMap.InitialData ({int key: bytes value}, map_abstract.go:33) as the flat image xe_add_map
+    takes, copied the way ArrayMap.Init does (emulator/maps_array.go:19-44): value k lands at
+    k*ValueSize and runs on into later entries when longer (keys applied in ascending order; Go's map
+    order is random and only matters for overlapping copies). Only ARRAY / PERCPU_ARRAY receive
+    InitialData (AbstractMapToVM, emulator/maps.go:101-108); other types get None."""
+    if data is None or d.type not in (MAP_ARRAY, MAP_PERCPU_ARRAY):
+        return None
+    size = d.value_size * d.max_entries
+    img = bytearray(size)
+    for k in sorted(data):
+        if not isinstance(k, int):
+            raise TypeError("the key type of the initial data must be an int")
+        v = bytes(data[k])
+        off = k * d.value_size
+        if k < 0 or off > size:
+            raise ValueError(f"initial data key {k} outside the map")
+        img[off:off + len(v)] = v[: size - off]
+    return bytes(img)
+
+
 def _stats_dict(s: N.BatchStats) -> dict:
     return {"packets": s.packets, "steps": s.steps, "status_count": list(s.status_count),
             "mode_used": s.mode_used, "conflict": s.conflict, "kernel_ms": s.kernel_ms,
@@ -113,7 +134,10 @@ class VM:
     def set_entrypoint(self, idx: int) -> None:
         self._check(self.lib.set_entrypoint(self.h, idx), "set entrypoint")
 
-    def add_map(self, d: MapDef, initial: bytes | np.ndarray | None = None) -> int:
+    def add_map(self, d: MapDef, initial: bytes | np.ndarray | dict | None = None) -> int:
+        """AddAbstractMap; `initial` is a flat image or an InitialData dict (initial_image)."""
+        if isinstance(initial, dict):
+            initial = initial_image(d, initial)
         md = N.MapDef(d.type, d.key_size, d.value_size, d.max_entries, d.flags)
         buf = None if initial is None else np.frombuffer(bytes(initial), dtype=np.uint8)
         idx = C.c_int32()
@@ -220,9 +244,64 @@ class VM:
         self._check(self.lib.map_apply_delta(self.h, m, lane, d_in, stream or None), "map apply delta")
 
     def footprint(self) -> np.ndarray:
+        """xe_footprint record of the last run: [flags, (read, add, widths) per map]."""
         nw = C.c_uint32()
         self._check(self.lib.footprint(self.h, None, 0, C.byref(nw)), "footprint")
         out = np.zeros(nw.value, dtype=np.uint64)
         self._check(self.lib.footprint(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), nw.value, C.byref(nw)),
                     "footprint")
         return out
+
+    def shard_check(self, fps: np.ndarray, nshards: int) -> tuple[bool, list[int]]:
+        """xe_shard_check over the concatenated footprint records of the shards, in shard order."""
+        fps = np.ascontiguousarray(fps, dtype=np.uint64)
+        nw = len(fps) // nshards
+        lanes = np.zeros(max(1, (nw - 1) // 3), dtype=np.uint32)
+        rc = self.lib.shard_check(fps.ctypes.data, nshards, nw, lanes.ctypes.data)
+        self._check(rc, "shard check")
+        return rc == 1, [int(x) for x in lanes]
+
+    def map_state_bytes(self, m: int) -> int:
+        b = C.c_uint64()
+        self._check(self.lib.map_state_bytes(self.h, m, C.byref(b)), "map state bytes")
+        return b.value
+
+    def map_state_export(self, m: int, d_out: int, stream: int = 0) -> None:
+        self._check(self.lib.map_state_export(self.h, m, d_out, stream or None), "map state export")
+
+    def map_state_import(self, m: int, d_in: int, stream: int = 0) -> None:
+        self._check(self.lib.map_state_import(self.h, m, d_in, stream or None), "map state import")
+
+
+class Multi:
+    """One process driving N devices (xe_multi_create / xe_run_batch_multi): vms[k] on its own device
+    (or sharing one, in tests), set up identically by the caller."""
+
+    def __init__(self, vms: list[VM]):
+        self.vms = vms
+        self.lib = vms[0].lib
+        arr = (C.c_void_p * len(vms))(*[v.h.value for v in vms])
+        h = C.c_void_p()
+        rc = self.lib.multi_create(arr, len(vms), C.byref(h))
+        if rc:
+            raise EmulatorError(rc, "multi create")
+        self.h = h
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.multi_destroy(self.h)
+            self.h = None
+
+    def run(self, d_umem: list[int], umem_len: list[int], d_desc: list[int], n: list[int],
+            d_results: list[int] | None = None, d_verdicts: list[int] | None = None) -> tuple[list[dict], bool]:
+        """Run shard k = (d_umem[k], d_desc[k], n[k]) on vms[k]; maps end equal to the single-VM result."""
+        G = len(self.vms)
+        ptrs = lambda xs: (C.c_void_p * G)(*[x or None for x in xs])
+        sts = (N.BatchStats * G)()
+        rep = C.c_uint32()
+        rc = self.lib.run_batch_multi(self.h, ptrs(d_umem), (C.c_uint64 * G)(*umem_len), ptrs(d_desc),
+                                      (C.c_uint32 * G)(*n), ptrs(d_results) if d_results else None,
+                                      ptrs(d_verdicts) if d_verdicts else None, sts, C.byref(rep))
+        if rc:
+            raise EmulatorError(rc, "run batch multi: " + self.lib.multi_last_error(self.h).decode(errors="replace"))
+        return [_stats_dict(s) for s in sts], bool(rep.value)

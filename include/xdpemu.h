@@ -228,20 +228,61 @@ int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc
                       xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);
 
 /* --- multi-GPU shard support: counter deltas for an RCCL all-reduce ---
+ * Shards are contiguous packet ranges run in index order: shard k holds the packets after those of
+ * shards < k, exactly the order of the reference's per-packet loop. Every shard's VM starts from the
+ * same map contents (and hash slot layout). After the runs, either the per-map deltas are summed
+ * (when xe_shard_check proves the effects commute across shards) or the shards are replayed in order,
+ * each starting from the map state the previous one ended with (xe_map_state_export / _import).
+ *
  * Values region of a map as a flat little-endian byte image (ARRAY: ValueSize*MaxEntries; HASH: the
  * device slot table's values, identical layout on every replica built the same way). */
 int xe_map_values_bytes(xe_vm* vm, int32_t map_idx, uint64_t* bytes);
-/* d_out (device, bytes) := current values - snapshot taken at the start of the last run, computed in
- * lanes of `lane` bytes (1, 2, 4, 8; 0 = the map's own xe_map_delta_lane): a narrow counter wraps at
- * its own width, so the cross-device sum must be taken in lanes of that width too */
+/* d_out (device) := current values - snapshot taken at the start of the last run, in lanes of `lane`
+ * bytes (1, 2, 4, 8; 0 = the width of the map's adds in the last run): a narrow counter wraps at its
+ * own width. Lane 2 deltas are written widened to u32 containers (2 * bytes long: RCCL has no 16-bit
+ * integer sum); every other lane is written at its own width (bytes long). */
 int xe_map_delta(xe_vm* vm, int32_t map_idx, uint32_t lane, void* d_out, void* stream);
-/* values := snapshot + d_in, in lanes of `lane` bytes (wrapping) */
+/* values := snapshot + d_in (same lanes and containers as xe_map_delta), wrapping per lane */
 int xe_map_apply_delta(xe_vm* vm, int32_t map_idx, uint32_t lane, const void* d_in, void* stream);
-/* width in bytes of the last run's adds into this map (1, 2, 4 or 8), 0 when there were none; more
- * than one width is an order-dependent run (replayed in order) and reports 8 */
+/* width in bytes of the last run's adds into this map (1, 2, 4 or 8), 0 when there were none, 8 when
+ * more than one width was used (such a run is order-dependent and was replayed in order) */
 int xe_map_delta_lane(xe_vm* vm, int32_t map_idx, uint32_t* lane_bytes);
-/* footprint masks of the last run, for cross-shard conflict checks: 2 u64 per map (read, atomic) + flags */
+/* Footprint record of the last run, for cross-shard checks: out[0] = XE_FPF_* flags, then for each
+ * map m = 1..nmaps three words: read mask, atomic-add mask (64 field positions of a value) and the
+ * width classes of its adds (bit 0: 1 B, 1: 2 B, 2: 4 B, 3: 8 B). nwords = 1 + 3 * nmaps. */
+#define XE_FPF_ORDERED 1    /* a lane needed a non-commutative map write */
+#define XE_FPF_SEQUENTIAL 2 /* the results come from the exact ordered replay (map writes in order) */
+#define XE_FPF_UNALIGNED 4  /* a map add was not aligned to its own width */
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords);
+/* Cross-shard exactness check over the footprints (xe_footprint records, nwords each) of ngpus
+ * shards given in shard order. Returns 1 when init + the sum of the per-map deltas equals the state
+ * one VM reaches over all shards in order and every shard saw the map values that VM would have
+ * shown it: no shard used the ordered path, no shard read a field an earlier shard added to, one add
+ * width per map everywhere, aligned adds. lanes[m - 1] receives the lane of map m (0 = no adds).
+ * Returns 0 when the shards must be replayed in order instead. */
+int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_t* lanes);
+/* Whole map state (values, hash slot records and entry count) as a device byte image, for the in-order
+ * shard replay: export on the shard that finished, import on the next (same map geometry). */
+int xe_map_state_bytes(xe_vm* vm, int32_t map_idx, uint64_t* bytes);
+int xe_map_state_export(xe_vm* vm, int32_t map_idx, void* d_out, void* stream);
+int xe_map_state_import(xe_vm* vm, int32_t map_idx, const void* d_in, void* stream);
+
+/* --- one process, N devices (SURVEY §8b xe_run_batch_multi): the Go host shards a batch over the
+ * GPUs of a node through the FFI alone. vms[k] runs on its own device with identical programs, maps
+ * and map contents (the caller sets each up the same way). Exchange over RCCL (xGMI) when the devices
+ * are distinct; VMs sharing a device (tests on one GPU) exchange through device kernels instead. */
+typedef struct xe_multi xe_multi;
+int xe_multi_create(xe_vm* const* vms, uint32_t ngpus, xe_multi** out);
+void xe_multi_destroy(xe_multi* m);
+/* Shard k: d_umem[k] (umem_len[k] bytes), d_desc[k] (n[k] descriptors), results/verdicts (may be
+ * NULL) — all on vms[k]'s device. Runs the shards concurrently, then makes every VM's maps equal to
+ * the single-VM result: delta all-reduce when xe_shard_check passes, otherwise the in-order replay
+ * (results of the replayed shards are rewritten). stats (may be NULL) receives ngpus records;
+ * *replayed (may be NULL) is 1 when the in-order replay ran. */
+int xe_run_batch_multi(xe_multi* m, void* const* d_umem, const uint64_t* umem_len, const void* const* d_desc,
+                       const uint32_t* n, void* const* d_results, void* const* d_verdicts, xe_batch_stats* stats,
+                       uint32_t* replayed);
+const char* xe_multi_last_error(const xe_multi* m);
 
 /* build / device info */
 const char* xe_version(void);

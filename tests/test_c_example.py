@@ -26,4 +26,19 @@ def test_c_example_builds_against_the_abi(example_bin):
 def test_c_example_runs_on_device(example_bin):
     r = subprocess.run([str(example_bin), "30000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "packets=30000 pass=30000 counts=10000,10000,10000" in r.stdout
+    assert "packets=30000 pass=30000 counts=11000,10000,10007" in r.stdout
+
+
+def test_c_example_runs_on_hostsim(built, tmp_path):
+    """The same C program linked against the host simulation build (CPU): the InitialData image
+    (ArrayMap.Init translation) and the batch run through the C ABI, without a GPU."""
+    sim = ROOT / "tests" / "hostsim"
+    lnk = tmp_path / "libxdpemu.so"
+    lnk.symlink_to(sim / "libxdpemu_hostsim.so")
+    out = tmp_path / "xdp_batch_sim"
+    r = subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", str(ROOT / "include"), str(ROOT / "examples" / "xdp_batch.c"),
+                        "-L", str(tmp_path), "-lxdpemu", f"-Wl,-rpath,{tmp_path}", "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(out), "3000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "packets=3000 pass=3000 counts=2000,1000,1007" in r.stdout

@@ -1,7 +1,9 @@
-"""N>1 path on CPU: world_size-2 `gloo` ranks each run a contiguous packet shard through the product
-(host-simulation build) on private map replicas, exchange counter deltas with one all-reduce (the
-bench's RCCL step), and must end with maps equal to the oracle's single VM over the whole
-batch (valid because the configs' map effects are commutative)."""
+"""N>1 path on CPU. world_size-2 `gloo` ranks each run a contiguous packet shard through the product's
+device logic (host-simulation build) on private map replicas and then make their maps exact with
+gobpfld_amd.shard.exchange_shards: a delta all-reduce when xe_shard_check proves the
+shards' effects commute, the in-order replay otherwise. Every rank must end with the maps — and the
+concatenated verdicts must equal the results — of the oracle's single VM over the whole batch.
+The single-process form (xe_run_batch_multi, two VMs in one process) is checked the same way."""
 import os
 import socket
 
@@ -14,6 +16,8 @@ import torch.multiprocessing as mp
 from gobpfld_amd import workloads as W
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = [("c2", 8192, None, True), ("c5", 8192, 4096, True), ("u32wrap", 64, None, True),
+         ("mixedwrap", 64, None, False), ("readvsadd", 256, None, False), ("rmw", 256, None, False)]
 
 
 def _free_port():
@@ -22,25 +26,45 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _batch(name, start, n):
+    if name in ("readvsadd", "rmw"):
+        # packets [0, n/2): byte 0 = 0 (adders); [n/2, n): byte 0 = 255 (readers)
+        from gobpfld_amd._native import np_dtypes
+        d_desc, _, _ = np_dtypes()
+        umem = np.zeros(n * 64, dtype=np.uint8)
+        descs = np.zeros(n, dtype=d_desc)
+        descs["addr"] = np.arange(n) * 64
+        descs["len"] = 64
+        umem[::64] = np.where(np.arange(start, start + n) >= _batch.total // 2, 255, 0)
+        return umem, descs
+    return W.build_batch("c2" if name in ("u32wrap", "mixedwrap") else name, start, n)
+
+
+_batch.total = 256
+
+
 def _rank(rank, world, port, name, n, cap, out_dir):
     import sys
     sys.path.insert(0, ROOT)
     from gobpfld_amd import _native as N
     from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import exchange_shards
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lib = N.Lib(os.path.join(ROOT, "tests", "hostsim", "libxdpemu_hostsim.so"), "xe_")
     vm = VM(Settings(), lib=lib)
     _setup(vm, name, cap)
     shard = n // world
-    umem, descs = W.build_batch("c2" if name == "u32wrap" else name, rank * shard, shard)
+    _batch.total = n
+    umem, descs = _batch(name, rank * shard, shard)
     ver = np.zeros(shard, dtype=np.uint32)
-    from gobpfld_amd.shard import allreduce_map_deltas
-    bufs = {m: torch.zeros(vm.map_values_bytes(m), dtype=torch.uint8) for m in vm.map_defs}
-    for step in range(2):  # two steps: deltas are per batch, against that batch's snapshot
-        vm.run_batch_device(umem.ctypes.data, umem.size, descs.ctypes.data, shard, d_verdicts=ver.ctypes.data)
-        allreduce_map_deltas(vm, list(vm.map_defs), bufs, dist)
+    run = lambda: vm.run_batch_device(umem.ctypes.data, umem.size, descs.ctypes.data, shard, d_verdicts=ver.ctypes.data)
+    exact = []
+    for step in range(2):  # two steps: each run's deltas / replay are against that run's start state
+        run()
+        exact.append(exchange_shards(vm, list(vm.map_defs), dist, run)["exact_sum"])
     np.save(os.path.join(out_dir, f"ver{rank}.npy"), ver)
+    np.save(os.path.join(out_dir, f"exact{rank}.npy"), np.array(exact))
     for m in vm.map_defs:
         with open(os.path.join(out_dir, f"map{m}_r{rank}.bin"), "wb") as f:
             f.write(_dump(vm, m))
@@ -56,22 +80,48 @@ def _dump(vm, m):
     return np.asarray(keys).tobytes() + b"|" + np.asarray(vals).tobytes()
 
 
-def _u32wrap_program():
-    """u32 counter (low half of a u64 value) starting at 0xFFFFFFF0: wraps within its 4-byte field."""
+def _wrap_program(mixed: bool):
+    """u32 counter (low half of a u64 value) starting at 0xFFFFFFF0 wraps within its 4-byte field;
+    `mixed` also adds to a u16 counter at offset 4 of the same value (two add widths on one map)."""
     from gobpfld_amd.asm import JEQ, Asm
     a = Asm()
     a.st(4, 10, -4, 0).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
     a.jmp(JEQ, 0, "out", imm=0)
     a.mov64(1, 1).xadd(4, 0, 0, 1)
+    if mixed:
+        a.mov64(1, 0x4000).xadd(2, 0, 4, 1)
     a.label("out").mov64(0, 2).exit()
     return a.assemble()
 
 
+def _role_program(rmw: bool):
+    """Packets whose byte 0 is < 128 add 1 to a u64 counter; the others return its value (readvsadd),
+    or (rmw) load, add and store it non-atomically — an ordered read-modify-write."""
+    from gobpfld_amd.asm import JEQ, JGT, Asm
+    a = Asm()
+    a.ldx(4, 6, 1, 0).ldx(1, 8, 6, 0)
+    a.st(4, 10, -4, 0).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "out", imm=0)
+    a.jmp(JGT, 8, "read", imm=127)
+    a.mov64(1, 1).xadd(8, 0, 0, 1).mov64(0, 2).exit()
+    a.label("read")
+    if rmw:
+        a.ldx(8, 1, 0, 0).add64(1, 3).stx(8, 0, 0, 1).mov64(0, src=1).exit()
+    else:
+        a.ldx(8, 0, 0, 0).exit()
+    a.label("out").mov64(0, 1).exit()
+    return a.assemble()
+
+
 def _setup(vm, name, cap):
-    if name == "u32wrap":
-        from gobpfld_amd.emulator import MAP_ARRAY, MapDef
-        vm.add_map(MapDef(MAP_ARRAY, 4, 8, 4), (0xFFFFFFF0).to_bytes(8, "little") + bytes(24))
-        vm.set_entrypoint(vm.add_raw_program(_u32wrap_program()))
+    from gobpfld_amd.emulator import MAP_ARRAY, MapDef
+    if name in ("u32wrap", "mixedwrap"):
+        vm.add_map(MapDef(MAP_ARRAY, 4, 8, 4), {0: (0xFFF0FFFFFFF0).to_bytes(8, "little")})
+        vm.set_entrypoint(vm.add_raw_program(_wrap_program(name == "mixedwrap")))
+        return
+    if name in ("readvsadd", "rmw"):
+        vm.add_map(MapDef(MAP_ARRAY, 4, 8, 1))
+        vm.set_entrypoint(vm.add_raw_program(_role_program(name == "rmw")))
         return
     for mdef, ents in W.workload_maps(name):
         mi = vm.add_map(mdef)
@@ -82,21 +132,60 @@ def _setup(vm, name, cap):
     vm.set_entrypoint(p)
 
 
-@pytest.mark.parametrize("name,n,cap", [("c2", 8192, None), ("c5", 8192, 4096), ("u32wrap", 64, None)])
-def test_two_rank_shards_equal_single_vm(tmp_path, oracle_lib, built, name, n, cap):
-    world = 2
-    mp.start_processes(_rank, args=(world, _free_port(), name, n, cap, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+def _oracle(oracle_lib, name, n, cap):
+    """Single VM over the whole batch, twice (the ranks run two steps)."""
     from gobpfld_amd.emulator import VM, Settings
     ov = VM(Settings(), lib=oracle_lib)
     _setup(ov, name, cap)
-    umem, descs = W.build_batch("c2" if name == "u32wrap" else name, 0, n)
+    _batch.total = n
+    umem, descs = _batch(name, 0, n)
     r1 = ov.run_batch(umem.copy(), descs)
     r2 = ov.run_batch(umem.copy(), descs)
+    dumps = {m: _dump(ov, m) for m in ov.map_defs}
+    ov.close()
+    return r2, dumps
+
+
+@pytest.mark.parametrize("name,n,cap,commutes", CASES, ids=[c[0] for c in CASES])
+def test_two_rank_shards_equal_single_vm(tmp_path, oracle_lib, built, name, n, cap, commutes):
+    world = 2
+    mp.start_processes(_rank, args=(world, _free_port(), name, n, cap, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    r2, dumps = _oracle(oracle_lib, name, n, cap)
     ver = np.concatenate([np.load(tmp_path / f"ver{r}.npy") for r in range(world)])
-    assert (ver == r2.verdicts).all() and (r1.verdicts == r2.verdicts).all()
-    for m in ov.map_defs:
-        want = _dump(ov, m)
+    assert (ver == r2.verdicts).all(), f"{name}: verdicts differ from the single VM"
+    for m, want in dumps.items():
         for r in range(world):
             assert (tmp_path / f"map{m}_r{r}.bin").read_bytes() == want, f"rank {r} map {m}"
-    ov.close()
+    exact = np.load(tmp_path / "exact0.npy")
+    assert exact.all() == commutes and exact.any() == commutes, (name, exact)
+
+
+@pytest.mark.parametrize("name,n,cap,commutes", CASES, ids=[c[0] for c in CASES])
+def test_single_process_multi_equals_single_vm(oracle_lib, hostsim_lib, name, n, cap, commutes):
+    """xe_run_batch_multi with two VMs in one process (host simulation: both on 'device' 0, so the
+    exchange takes the device-kernel path instead of RCCL)."""
+    from gobpfld_amd.emulator import Multi, VM, Settings
+    G = 2
+    vms = [VM(Settings(), lib=hostsim_lib) for _ in range(G)]
+    for v in vms:
+        _setup(v, name, cap)
+    mu = Multi(vms)
+    shard = n // G
+    _batch.total = n
+    bufs = [_batch(name, k * shard, shard) for k in range(G)]
+    vers = [np.zeros(shard, dtype=np.uint32) for _ in range(G)]
+    reps = []
+    for step in range(2):
+        _, rep = mu.run([u.ctypes.data for u, _ in bufs], [u.size for u, _ in bufs], [d.ctypes.data for _, d in bufs],
+                        [shard] * G, d_verdicts=[v.ctypes.data for v in vers])
+        reps.append(rep)
+    r2, dumps = _oracle(oracle_lib, name, n, cap)
+    assert (np.concatenate(vers) == r2.verdicts).all()
+    for m, want in dumps.items():
+        for k, v in enumerate(vms):
+            assert _dump(v, m) == want, f"vm {k} map {m}"
+    assert reps == [not commutes] * 2
+    mu.close()
+    for v in vms:
+        v.close()

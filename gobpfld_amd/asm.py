@@ -54,6 +54,8 @@ class Asm:
         for pc, (op, dst, src, off, imm) in enumerate(self.slots):
             if isinstance(off, str):
                 off = self.labels[off] - pc - 1
+            if isinstance(imm, str):  # bpf-to-bpf call: the relative target is in imm
+                imm = self.labels[imm] - pc - 1
             if not -32768 <= off <= 32767:
                 raise ValueError("jump offset out of range")
             out.append(raw(op, dst, src, off, imm))
@@ -123,6 +125,9 @@ class Asm:
 
     def call(self, helper):
         return self.emit(JMP | CALL, 0, 0, 0, helper)
+
+    def call_bpf(self, target):  # BPF_PSEUDO_CALL (src = 1): PC += imm (emulator/inst_call_bpf.go:41)
+        return self.emit(JMP | CALL, 0, 1, 0, target)
 
     def exit(self):
         return self.emit(JMP | EXIT)

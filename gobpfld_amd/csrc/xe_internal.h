@@ -18,6 +18,18 @@
 #define XE_HD static inline
 #endif
 
+// Tuning knobs (A/B experiments through the environment) exist only in the debug build
+// (-DXE_TUNING: gobpfld_amd/libxdpemu_tuning.so, gobpfld_amd/build.py build_tuning); the product library
+// never reads the environment.
+#if !defined(__HIPCC_RTC__)
+#if defined(XE_TUNING)
+#include <stdlib.h>
+static inline const char* xe_tuning_env(const char* name) { return getenv(name); }
+#else
+static inline const char* xe_tuning_env(const char*) { return nullptr; }
+#endif
+#endif
+
 // ---------------------------------------------------------------- micro-ops
 // One 16-byte record per eBPF instruction slot (the LD_IMM64 filler keeps its own slot, exactly
 // as ebpf.Decode emits a Nop, ebpf/decode.go:34), so PCs stay identical to the reference's.
@@ -39,7 +51,7 @@ enum XeUopClass : uint8_t {
   U_ATOMIC,     // emulator/inst_atomic.go:20-65
   U_HELPER,     // CallHelper with a known helper id (imm)
   U_CALLX,      // CallHelperIndirect; dst = register holding the helper id
-  U_CALLBPF,    // bpf-to-bpf call (device: XE_ST_UNSUPPORTED in this round)
+  U_CALLBPF,    // bpf-to-bpf call, emulator/inst_call_bpf.go (general lane model)
   U_NCLASSES
 };
 
@@ -66,11 +78,14 @@ XE_HD int uop_size(const XeUop& u) { return 1 << ((u.fl >> 4) & 3); }
 // ---------------------------------------------------------------- memory handles
 // A pointer register's Memory is encoded in 32 bits: class (3) | map index (6) | slot (23).
 #define XE_H_CLS_SHIFT 29
-#define XE_H_PKT 0u
-#define XE_H_CTX 1u
-#define XE_H_STACK 2u
-#define XE_H_ARRAY 3u
-#define XE_H_HASH 4u
+#define XE_H_PKT 0u     // the packet ByteMemory
+#define XE_H_CTX 1u     // the xdp_md ctx ValueMemory
+#define XE_H_STACK 2u   // stack frame ValueMemory; map field = frame index (StackFrames[i])
+#define XE_H_ARRAY 3u   // ArrayMap memory of map m
+#define XE_H_HASH 4u    // HASH value (slot) / LRU_HASH value (value id) of map m
+#define XE_H_VCLONE 5u  // general model: a lane-private ValueMemory clone (Registers.Clone at a call)
+#define XE_H_BMEM 6u    // general model: a lane-private ByteMemory (a clone, or a popped element copy)
+#define XE_H_QVAL 7u    // QUEUE / STACK element (slot = element id) or PERF event (slot = event index)
 #define XE_H_MAX_MAPS 63
 #define XE_H_SLOT_BITS 23
 XE_HD uint32_t xe_h_make(uint32_t cls, uint32_t map, uint32_t slot) {
@@ -81,13 +96,16 @@ XE_HD uint32_t xe_h_map(uint32_t h) { return (h >> XE_H_SLOT_BITS) & 63u; }
 XE_HD uint32_t xe_h_slot(uint32_t h) { return h & ((1u << XE_H_SLOT_BITS) - 1u); }
 
 // ---------------------------------------------------------------- device maps
-enum : uint32_t { XE_DM_NONE = 0, XE_DM_ARRAY = 1, XE_DM_HASH = 2, XE_DM_OTHER = 3 };
+enum : uint32_t { XE_DM_NONE = 0, XE_DM_ARRAY = 1, XE_DM_HASH = 2, XE_DM_LRU = 3, XE_DM_LIST = 4, XE_DM_PERF = 5 };
 #define XE_SLOT_FULL 1u
 #define XE_SLOT_VLEN0 2u   // HashMap value whose backing became nil (maps_hash.go:108-115)
+#define XE_SLOT_TOMB 4u    // LRU_HASH: evicted / deleted slot (probe chains run through it)
+#define XE_NONE 0xffffffffu
 #define XE_MAX_KEY 64      // device hash keys up to 64 bytes (8 words)
 
 struct XeDevMap {
   uint32_t kind;        // XE_DM_*
+  uint32_t btype;       // bpftypes.BPFMapType (XE_MAP_*): TailCall wants a PROG_ARRAY
   uint32_t key_size;
   uint32_t value_size;
   uint32_t max_entries;
@@ -105,6 +123,20 @@ struct XeDevMap {
   uint64_t rep_stride;  // bytes between replicas
   uint32_t nrep;        // 1 = adds go to vals directly
   uint32_t rwords;      // HASH: u64 words per slot record (power of two >= 1 + kwords)
+  // LRU_HASH / QUEUE / STACK / PERF_EVENT_ARRAY (ordered maps; the general lane model only)
+  //   LRU:  keys = slot records ([0] = state | value id << 32), vals = value pool (pool_cap values),
+  //         link = prev/next value ids (UsageList as a linked list), elen = value length (0: nil backing),
+  //         hdr = {head (MRU), tail (LRU), count, next value id}
+  //   LIST: vals = element pool, elen = element length, link = the list (ring of list_cap ids for a
+  //         queue), hdr = {head, count, next element id, 0, is_stack}
+  //   PERF: vals = event bytes (data_cap), rec = {offset, length} per event, hdr = {count, data used}
+  uint64_t* hdr;
+  uint32_t* link;
+  uint32_t* elen;
+  uint64_t* rec;
+  uint32_t pool_cap;
+  uint32_t list_cap;
+  uint64_t data_cap;
 };
 
 XE_HD uint32_t xe_hash_rwords(uint32_t kwords) {
@@ -131,6 +163,7 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 
 // kernel-side status of a lane beyond the public XE_ST_*
 #define XE_ST_INTERNAL_ORDERED 6
+#define XE_ST_INTERNAL_CAPACITY 7  // general model: the lane's arena ran out (the host replays with more)
 
 // replica record words: [0] steps, [1..8] status histogram, [9..12] atomic width classes (4 bits per
 // map: 1, 2, 4, 8 bytes), [16 + 2m] read mask and [17 + 2m] atomic mask of map m
@@ -138,8 +171,27 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 
 // flags word bits (device -> host)
 #define XE_FLAG_ORDERED 1u   // a lane needed a non-commutative map write in parallel mode
-#define XE_FLAG_CAPACITY 2u
+#define XE_FLAG_CAPACITY 2u   // a lane ran out of its arena (general model): the host replays with more
 #define XE_FLAG_UNALIGNED 4u  // a map add not aligned to its own width (cross-shard delta lanes inexact)
+
+// General lane model (xe_interp.h, XE_GEN): the Go object model without fixed limits, per lane in a
+// device arena. Lanes are interleaved (element e of lane l at [e * nl + l]) so the lanes of a wave
+// touching the same element touch one contiguous line. Capacities are per lane; running out raises
+// XE_FLAG_CAPACITY and the host replays the batch in order with a larger arena (never a packet status).
+struct XeGen {
+  uint8_t* base;
+  uint32_t nl;       // lanes sharing the arena
+  uint32_t nobj;     // object ids < nobj (0 = nil, 1..6 = the xdp_md objects)
+  uint32_t nframes;  // stack frames kept per lane (1, or 8 = MaxStackFrames with bpf-to-bpf calls)
+  uint32_t nvc;      // ValueMemory clones
+  uint32_t nbm;      // private ByteMemories
+  uint32_t nkey;     // key scratch bytes (hash keys longer than XE_MAX_KEY)
+  uint64_t nbytes;   // private byte arena per lane
+  uint64_t o_ov, o_oh, o_ot, o_ofree, o_mark, o_frm, o_ctx, o_vc, o_vcinfo, o_vfree, o_bm, o_bfree, o_pres, o_key;
+  uint64_t o_bytes;  // per-lane contiguous: lane l's bytes at o_bytes + l * nbytes
+  uint32_t mark_words;  // u32 mark words per lane: objects, then VCs, then BMs
+  uint32_t pad;
+};
 
 // per-launch parameters
 struct XeParams {
@@ -165,4 +217,11 @@ struct XeParams {
   unsigned long long* rep;
   uint32_t nrep;
   uint32_t rep_words;
+  // every program of the VM, concatenated (tail calls switch programs, emulator/helper_functions.go:133-210)
+  const XeUop* progs;
+  const int32_t* prog_off;  // [0..nprogs]: program p at progs + prog_off[p], prog_off[0] unused
+  const int32_t* prog_lens;
+  uint32_t nprogs;          // len(vm.Programs) - 1
+  int32_t entry;            // PI at Reset (SetEntrypoint)
+  XeGen gen;
 };

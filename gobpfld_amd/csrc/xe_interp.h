@@ -7,23 +7,29 @@
 //
 // Register/memory model — an exact encoding of gobpfld's object model (emulator/registers.go,
 // emulator/memory.go):
-//   * R0..R10 live in VGPR arrays indexed by the (wave-uniform) micro-op fields: value (i64),
-//     memory handle (u32) and a tag (kind | readonly | alias id).
-//   * Objects stored in a ValueMemory (the 24-byte xdp_md ctx and the 256-byte stack frame) live in
-//     a per-lane object table (ids 1..63); ValueMemory bytes hold object ids (0 = nil).
+//   * R0..R10 are {value (i64), memory handle (u32), tag (kind | readonly | alias id)}.
+//   * Objects stored in a ValueMemory (the 24-byte xdp_md ctx, 256-byte stack frames, clones of
+//     either) live in a per-lane object table; ValueMemory bytes hold object ids (0 = nil).
 //   * LDX from a ValueMemory makes the register alias the stored object (emulator/memory.go:37-52,
 //     emulator/inst_load.go:112); in-place ALU ops on an aliased register update the object and
 //     every other register aliasing it, exactly like mutating the shared Go object.
-//   * Stack/ctx byte maps reset lazily with a dirty-word mask (Reset nils 2,048 slots per packet,
-//     emulator/vm.go:229-239; here one VGPR write).
+//
+// Two lane models share every handler below:
+//   * fields model (XE_MEM_FIELDS, per-program kernels of programs that provably fit): the object
+//     table, frame 0 and the ctx are named fields that fold into VGPRs — the fast path;
+//   * general model (XE_GEN, everything else: loops, > 57 live objects, bpf-to-bpf calls with the
+//     frames 1..7 and the Registers.Clone deep copies they make, tail calls, nil registers, the
+//     LRU / queue / stack / perf maps): the same objects in a per-lane device arena (XeGen) with
+//     mark-sweep collection; running out of arena is never a packet status — the host replays the
+//     batch in order with a larger arena.
 //
 // Maps: ARRAY memory and HASH slot values are device-global. In parallel mode only commutative map
 // effects are executed (atomic adds); a lane that would perform a non-atomic map write aborts the
 // batch (XE_FLAG_ORDERED) and the host re-runs it in exact packet order (sequential mode). Lanes
 // record read / atomic footprints per map so the host can verify order-independence.
 //
-// The same source builds the gfx950 kernel (xe_kernel.hip) and, with XE_HOSTSIM, a wave-size-1 host
-// simulation used only by CPU tests to exercise this logic before it reaches the GPU.
+// The same source builds the gfx950 kernels (xe_kernel.hip, per-program kernels via xe_jit.cpp) and,
+// with XE_HOSTSIM, a wave-size-1 host simulation used only by CPU tests to exercise this logic.
 #pragma once
 #include "xe_internal.h"
 
@@ -84,13 +90,32 @@ XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return __
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 #endif
 
+#if defined(XE_MEM_FIELDS)
+#define XE_GEN 0
+#else
+#define XE_GEN 1
+#endif
+// Rare, large paths of the general model stay out of line (collection, clones, calls, ordered maps),
+// so the interpreter's dispatch loop keeps its registers.
+#if defined(__HIPCC__)
+#define XE_COLD __device__ __attribute__((noinline))
+#else
+#define XE_COLD static
+#endif
+
 // map kinds present in the VM (the per-program kernel sets these from the VM's maps, so helper paths
-// for absent kinds are compiled out; the interpreter keeps both)
+// for absent kinds are compiled out; the interpreter keeps all)
 #ifndef XE_HAS_ARRAY
 #define XE_HAS_ARRAY 1
 #endif
 #ifndef XE_HAS_HASH
 #define XE_HAS_HASH 1
+#endif
+#if !XE_GEN
+#undef XE_HAS_ORDERED
+#define XE_HAS_ORDERED 0  // LRU / queue / stack / perf maps and their helpers: general model only
+#elif !defined(XE_HAS_ORDERED)
+#define XE_HAS_ORDERED 1
 #endif
 
 // maps whose read / atomic footprints a lane keeps in registers (the rest OR straight into the wave's
@@ -136,15 +161,20 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_IS_PANIC(e) (XE_EV_CLASS(e) == XE_EV_PANIC)
 
 #define XE_NOBJ 64
-#define XE_STACK_WORDS 32   // 256-byte frame 0
-#define XE_CTX_WORD0 32     // ctx bytes 0..23 = words 32..34
+#define XE_STACK_WORDS 32   // 256-byte frame 0 (fields model)
+#define XE_CTX_WORD0 32     // ctx bytes 0..23 = words 32..34 (fields model)
 #define XE_NWORDS 35
 #define XE_CTX_LEN 24
+#define XE_FRAME 256        // DefaultVMSettings().StackFrameSize (emulator/vm.go:291-296)
+#define XE_MAX_FRAMES 8     // DefaultVMSettings().MaxStackFrames
 
-// tag layout
+// tag layout: kind (2 bits) | readonly (bit 2) | alias object id << 8
 #define XE_T_KIND(t) ((t) & 3u)
 #define XE_T_RO 4u
-#define XE_T_ALIAS(t) (((t) >> 8) & 63u)
+#define XE_T_ALIAS(t) ((t) >> 8)
+#define XE_ISPTR(t) (XE_T_KIND(t) == XE_KIND_MEMPTR || XE_T_KIND(t) == XE_KIND_FRAMEPTR)
+// a method call on a nil RegisterValue panics (only the general model has nil registers)
+#define XE_NILCHK(R) do { if (XE_GEN && XE_T_KIND((R).t) == XE_KIND_NIL) return XE_EV_PANIC | XE_P_NIL_DEREF; } while (0)
 
 XE_DEV int64_t xe_wadd(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
 XE_DEV int64_t xe_wmul(int64_t a, int64_t b) { return int64_t(uint64_t(a) * uint64_t(b)); }
@@ -157,29 +187,13 @@ XE_DEV uint64_t xe_ctx_default_word(int w) {
        : 0x0606060605050505ull;
 }
 
-// Per-lane memory: object table (ids 1..63; 1..6 are the xdp_md ctx objects, materialised lazily)
-// and the ValueMemory byte maps (object ids), reset lazily via XeLane::dirty. Accessed only through
-// the xm_* functions below. The interpreter keeps them in scratch (dynamic indices); a per-program
-// kernel whose accesses are statically indexed defines XE_MEM_FIELDS and supplies XeMem as named
-// fields with switch accessors (xe_jit.cpp), so the whole table lives in VGPRs after SROA.
-#if !defined(XE_MEM_FIELDS)
-#define XE_OBJ_LIMIT XE_NOBJ
-struct XeMem {
-  int64_t ov[XE_NOBJ];
-  uint32_t oh[XE_NOBJ];
-  uint32_t ot[XE_NOBJ];
-  uint64_t bm[XE_NWORDS];
-};
-XE_DEV int64_t xm_ov(const XeMem& M, int i) { return M.ov[i]; }
-XE_DEV uint32_t xm_oh(const XeMem& M, int i) { return M.oh[i]; }
-XE_DEV uint32_t xm_ot(const XeMem& M, int i) { return M.ot[i]; }
-XE_DEV void xm_set_obj(XeMem& M, int i, int64_t v, uint32_t h, uint32_t t) { M.ov[i] = v; M.oh[i] = h; M.ot[i] = t; }
-XE_DEV void xm_set_ov(XeMem& M, int i, int64_t v) { M.ov[i] = v; }
-XE_DEV uint64_t xm_bm(const XeMem& M, int w) { return M.bm[w]; }
-XE_DEV void xm_set_bm(XeMem& M, int w, uint64_t v) { M.bm[w] = v; }
-#define XE_UNROLL_VM _Pragma("unroll 1")
-#else
+// Fields model: the per-program kernel (xe_jit.cpp emit_mem_fields) supplies XeMem as named fields
+// with the xm_* accessors: object ids 1..XE_OBJ_LIMIT-1 (its static bound), 35 byte-map words
+// (frame 0 + ctx, 8 object ids per word).
+#if !XE_GEN
 #define XE_UNROLL_VM _Pragma("unroll")
+#else
+#define XE_UNROLL_VM _Pragma("unroll 1")
 #endif
 
 // Per-wave accumulator table of deferred map adds (parallel mode only), in LDS: XE_ACC direct-mapped
@@ -221,13 +235,26 @@ typedef unsigned int xe_v16u __attribute__((ext_vector_type(16)));
 struct XeLane {
   // registers R0..R10 (see reg_get/reg_put)
   XE_REG_DECL
-  // dynamically indexed lane memory (object table, byte maps): a separate struct so that the
-  // register fields above stay splittable into VGPRs (SROA gives up on aggregates with any
-  // variable-indexed member)
+#if !XE_GEN
+  // fields model: object table + frame 0 / ctx byte maps (a separate struct so that the register
+  // fields above stay splittable into VGPRs)
   struct XeMem* mem;
   uint64_t oused;     // allocated object ids
-  uint64_t odef;      // ids 1..6 still holding their ctx default
   uint64_t dirty;     // ValueMemory words written since Reset
+#else
+  const XeGen* G;     // arena layout (P.gen, in the kernel-argument segment: scalar loads)
+  uint32_t gl;        // this lane's slot in the arena
+  uint32_t onext, ofree;  // object ids: bump pointer, free-list length
+  uint32_t vnext, vfree;  // ValueMemory clones
+  uint32_t bnext, bfree;  // private ByteMemories
+  uint64_t bused;         // private byte arena in use
+  uint64_t fdirty[2];     // frame f, group g (16 slots): bit f * 16 + g = written since the frame was wiped
+  uint32_t ctxdirty;      // ctx slot s written (otherwise it holds the default object 1 + s / 4)
+  uint32_t npres;         // PreservedRegisters depth = R10's frame index
+  int32_t pi;             // program index (Registers.PI)
+  uint32_t npristine;     // private ByteMemories still reading through to their source
+#endif
+  uint64_t odef;      // ids 1..6 still holding their ctx default
   // packet
   uint8_t* pkt;
   int64_t plen;
@@ -249,7 +276,6 @@ struct XeLane {
   uint32_t awidth;          // atomic width classes used on maps 1..4 (4 bits per map)
   XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
 };
-
 
 // ------------------------------------------------------------------ registers
 // By-value element access on the vector members: the index is wave-uniform (micro-op fields), so
@@ -280,7 +306,15 @@ XE_DEV void reg_put(XeLane& L, int i, const XeReg& r) {
 }
 #endif
 
-// ------------------------------------------------------------------ object table
+// ------------------------------------------------------------------ object table + ValueMemory
+// A ValueMemory region: fields model r = first byte-map word (frame 0 = 0, ctx = 32); general model
+// r = 0..7 frame, 8 ctx, 16 + k ValueMemory clone k.
+struct XeVR {
+  int r;
+  int64_t len;
+};
+
+#if !XE_GEN
 XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& t) {
   if ((L.odef >> id) & 1ull) {
     // xdp_md objects: data, data_end, data_meta = MemoryPtr{pkt}, then 3 IMMs
@@ -293,13 +327,10 @@ XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& 
   h = xm_oh(*L.mem, id);
   t = xm_ot(*L.mem, id);
 }
-
 XE_DEV void obj_set(XeLane& L, int id, int64_t v, uint32_t h, uint32_t t) {
   xm_set_obj(*L.mem, id, v, h, t);
   L.odef &= ~(1ull << id);
 }
-
-// in-place value update of object `id` (RegisterValue.Assign on a shared object)
 XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
   if ((L.odef >> id) & 1ull) {
     int64_t ov; uint32_t oh, ot;
@@ -309,7 +340,6 @@ XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
     xm_set_ov(*L.mem, id, v);
   }
 }
-
 XE_DEV uint64_t bm_word(const XeLane& L, int w) {
   if ((L.dirty >> w) & 1ull) return xm_bm(*L.mem, w);
   return w >= XE_CTX_WORD0 ? xe_ctx_default_word(w) : 0ull;
@@ -318,37 +348,256 @@ XE_DEV void bm_set_word(XeLane& L, int w, uint64_t v) {
   xm_set_bm(*L.mem, w, v);
   L.dirty |= 1ull << w;
 }
-
-// mark-sweep collection of object ids when the table is full (a per-program kernel with the table in
-// registers is only built when no path can fill it: XE_OBJ_LIMIT >= 7 + stores on the longest path)
-#if !defined(XE_MEM_FIELDS)
-XE_DEV void obj_gc(XeLane& L) {
-  uint64_t marks = 1ull;
-#pragma unroll 1
-  for (int w = 0; w < XE_NWORDS; w++) {
-    uint64_t word = bm_word(L, w);
-#pragma unroll 1
-    for (int b = 0; b < 8; b++) marks |= 1ull << ((word >> (8 * b)) & 63u);
-  }
-#pragma unroll
-  for (int r = 0; r < 10; r++) {
-    uint32_t a = XE_T_ALIAS(reg_get(L, r).t);
-    if (a) marks |= 1ull << a;
-  }
-  marks |= 1ull;
-  L.oused = marks;
-}
-#endif
-
+// the per-program kernel only uses this model when no path can exhaust the ids (xe_jit.cpp)
 XE_DEV int obj_alloc(XeLane& L) {
-#if !defined(XE_MEM_FIELDS)
-  if (L.oused == ~0ull) obj_gc(L);
-#endif
   if (L.oused == ~0ull) return -1;
   int id = __builtin_ctzll(~L.oused);
   L.oused |= 1ull << id;
   return id;
 }
+XE_DEV XeVR vmem_region(const XeLane&, uint32_t h) {
+  return xe_h_cls(h) == XE_H_CTX ? XeVR{XE_CTX_WORD0, XE_CTX_LEN} : XeVR{0, XE_FRAME};
+}
+XE_DEV int vmem_id(const XeLane& L, XeVR R, int64_t off) {
+  uint64_t word = bm_word(L, R.r + int(off >> 3));
+  return int((word >> (8 * (off & 7))) & 0xffu);
+}
+XE_DEV int vmem_fill(XeLane& L, XeVR R, int64_t off, int size, int id) {
+  int64_t end = off + size;
+  int w0 = int(off >> 3), w1 = int((end - 1) >> 3);
+  XE_UNROLL_VM
+  for (int w = w0; w <= w1; w++) {
+    int64_t lo = off > int64_t(w) * 8 ? off - int64_t(w) * 8 : 0;
+    int64_t hi = end < int64_t(w + 1) * 8 ? end - int64_t(w) * 8 : 8;
+    uint64_t mask = (hi - lo == 8) ? ~0ull : (((1ull << (8 * (hi - lo))) - 1ull) << (8 * lo));
+    uint64_t word = bm_word(L, R.r + w);
+    word = (word & ~mask) | ((uint64_t(id) * 0x0101010101010101ull) & mask);
+    bm_set_word(L, R.r + w, word);
+  }
+  return 0;
+}
+#else  // ---- general model: the arena
+template <class T>
+XE_DEV XE_GP(T) gat(const XeLane& L, uint64_t field, uint64_t elem) {
+  return (XE_GP(T))(L.G->base + field + (elem * L.G->nl + L.gl) * sizeof(T));
+}
+XE_DEV XE_GP(uint8_t) lane_bytes(const XeLane& L) { return (XE_GP(uint8_t))(L.G->base + L.G->o_bytes + uint64_t(L.gl) * L.G->nbytes); }
+
+XE_DEV void obj_get(const XeLane& L, int id, int64_t& v, uint32_t& h, uint32_t& t) {
+  if (id < 64 && ((L.odef >> id) & 1ull)) {
+    h = id <= 3 ? xe_h_make(XE_H_PKT, 0, 0) : 0u;
+    t = id <= 3 ? uint32_t(XE_KIND_MEMPTR) : uint32_t(XE_KIND_IMM);
+    v = id == 2 ? L.plen : id == 4 ? int64_t(L.ingress) : id == 5 ? int64_t(L.rxq) : 0;
+    return;
+  }
+  v = *gat<int64_t>(L, L.G->o_ov, uint32_t(id));
+  h = *gat<uint32_t>(L, L.G->o_oh, uint32_t(id));
+  t = *gat<uint32_t>(L, L.G->o_ot, uint32_t(id));
+}
+XE_DEV void obj_set(XeLane& L, int id, int64_t v, uint32_t h, uint32_t t) {
+  *gat<int64_t>(L, L.G->o_ov, uint32_t(id)) = v;
+  *gat<uint32_t>(L, L.G->o_oh, uint32_t(id)) = h;
+  *gat<uint32_t>(L, L.G->o_ot, uint32_t(id)) = t;
+  if (id < 64) L.odef &= ~(1ull << id);
+}
+XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
+  if (id < 64 && ((L.odef >> id) & 1ull)) {
+    int64_t ov; uint32_t oh, ot;
+    obj_get(L, id, ov, oh, ot);
+    obj_set(L, id, v, oh, ot);
+  } else {
+    *gat<int64_t>(L, L.G->o_ov, uint32_t(id)) = v;
+  }
+}
+
+// -- ValueMemory regions
+XE_DEV uint32_t vc_len(const XeLane& L, uint32_t k) { return *gat<uint32_t>(L, L.G->o_vcinfo, k) & 0xffffu; }
+XE_DEV uint32_t vc_src(const XeLane& L, uint32_t k) { return *gat<uint32_t>(L, L.G->o_vcinfo, k) >> 16; }  // XE_H_CTX / XE_H_STACK
+XE_DEV XeVR vmem_region(const XeLane& L, uint32_t h) {
+  const uint32_t c = xe_h_cls(h);
+  if (c == XE_H_CTX) return XeVR{8, XE_CTX_LEN};
+  if (c == XE_H_VCLONE) return XeVR{16 + int(xe_h_slot(h)), int64_t(vc_len(L, xe_h_slot(h)))};
+  return XeVR{int(xe_h_map(h)), XE_FRAME};
+}
+XE_DEV bool frame_group_dirty(const XeLane& L, int f, int g) {
+  const int bit = f * 16 + g;
+  return (L.fdirty[bit >> 6] >> (bit & 63)) & 1ull;
+}
+XE_DEV int vmem_id(const XeLane& L, XeVR R, int64_t off) {
+  if (R.r < 8) {
+    if (!frame_group_dirty(L, R.r, int(off >> 4))) return 0;
+    return *gat<uint16_t>(L, L.G->o_frm, uint64_t(R.r) * XE_FRAME + uint64_t(off));
+  }
+  if (R.r == 8) {
+    if (!((L.ctxdirty >> off) & 1u)) return 1 + int(off >> 2);
+    return *gat<uint16_t>(L, L.G->o_ctx, uint64_t(off));
+  }
+  return *gat<uint16_t>(L, L.G->o_vc, uint64_t(R.r - 16) * XE_FRAME + uint64_t(off));
+}
+XE_DEV void vmem_set(XeLane& L, XeVR R, int64_t off, int id) {
+  if (R.r < 8) {
+    const int g = int(off >> 4);
+    if (!frame_group_dirty(L, R.r, g)) {  // the group held nil since the frame was wiped
+#pragma unroll 1
+      for (int s = 0; s < 16; s++) *gat<uint16_t>(L, L.G->o_frm, uint64_t(R.r) * XE_FRAME + uint64_t(g * 16 + s)) = 0;
+      const int bit = R.r * 16 + g;
+      L.fdirty[bit >> 6] |= 1ull << (bit & 63);
+    }
+    *gat<uint16_t>(L, L.G->o_frm, uint64_t(R.r) * XE_FRAME + uint64_t(off)) = uint16_t(id);
+  } else if (R.r == 8) {
+    *gat<uint16_t>(L, L.G->o_ctx, uint64_t(off)) = uint16_t(id);
+    L.ctxdirty |= 1u << off;
+  } else {
+    *gat<uint16_t>(L, L.G->o_vc, uint64_t(R.r - 16) * XE_FRAME + uint64_t(off)) = uint16_t(id);
+  }
+}
+XE_DEV int vmem_fill(XeLane& L, XeVR R, int64_t off, int size, int id) {
+#pragma unroll 1
+  for (int i = 0; i < size; i++) vmem_set(L, R, off + i, id);
+  return 0;
+}
+
+// -- private ByteMemories: {source handle, materialised offset (XE_NONE while it reads through), length,
+//    region | map << 8 for the parity record}
+#define XE_BM_SRC 0
+#define XE_BM_MAT 1
+#define XE_BM_LEN 2
+#define XE_BM_INFO 3
+XE_DEV XE_GP(uint32_t) bm_field(const XeLane& L, uint32_t k, int f) { return gat<uint32_t>(L, L.G->o_bm, uint64_t(k) * 4 + uint64_t(f)); }
+
+// -- preserved registers (bpf-to-bpf calls): entry e = {pc, then R6..R9 as (v lo, v hi, h, t)}
+XE_DEV XE_GP(uint32_t) pres_word(const XeLane& L, uint32_t e, int w) { return gat<uint32_t>(L, L.G->o_pres, uint64_t(e) * 17 + uint64_t(w)); }
+XE_DEV XeReg pres_get(const XeLane& L, uint32_t e, int r) {
+  const int w = 1 + 4 * r;
+  return XeReg{int64_t(uint64_t(*pres_word(L, e, w)) | (uint64_t(*pres_word(L, e, w + 1)) << 32)), *pres_word(L, e, w + 2),
+               *pres_word(L, e, w + 3)};
+}
+XE_DEV void pres_put(XeLane& L, uint32_t e, int r, const XeReg& R) {
+  const int w = 1 + 4 * r;
+  *pres_word(L, e, w) = uint32_t(uint64_t(R.v));
+  *pres_word(L, e, w + 1) = uint32_t(uint64_t(R.v) >> 32);
+  *pres_word(L, e, w + 2) = R.h;
+  *pres_word(L, e, w + 3) = R.t;
+}
+
+// -- mark-sweep collection of object ids, ValueMemory clones and private ByteMemories. Roots: R0-R9,
+//    the preserved registers, frames 0..depth, the ctx; then to a fixed point: the slots of live
+//    clones, the memories of live pointer objects, the sources of live ByteMemory clones.
+XE_DEV XE_GP(uint32_t) mark_word(const XeLane& L, uint32_t w) { return gat<uint32_t>(L, L.G->o_mark, w); }
+XE_DEV bool mark_set(XeLane& L, uint32_t bit) {  // returns true when newly marked
+  XE_GP(uint32_t) p = mark_word(L, bit >> 5);
+  const uint32_t m = 1u << (bit & 31);
+  if (*p & m) return false;
+  *p |= m;
+  return true;
+}
+XE_DEV bool mark_get(const XeLane& L, uint32_t bit) { return (*mark_word(L, bit >> 5) >> (bit & 31)) & 1u; }
+XE_DEV uint32_t vc_bit(const XeLane& L, uint32_t k) { return ((L.G->nobj + 31) & ~31u) + k; }
+XE_DEV uint32_t bm_bit(const XeLane& L, uint32_t k) { return ((L.G->nobj + 31) & ~31u) + ((L.G->nvc + 31) & ~31u) + k; }
+XE_DEV bool mark_handle(XeLane& L, uint32_t h) {
+  const uint32_t c = xe_h_cls(h);
+  if (c == XE_H_VCLONE) return mark_set(L, vc_bit(L, xe_h_slot(h)));
+  if (c == XE_H_BMEM) return mark_set(L, bm_bit(L, xe_h_slot(h)));
+  return false;
+}
+XE_DEV bool mark_obj(XeLane& L, int id) { return id > 0 && mark_set(L, uint32_t(id)); }
+
+XE_COLD void gen_gc(XeLane& L) {
+#pragma unroll 1
+  for (uint32_t w = 0; w < L.G->mark_words; w++) *mark_word(L, w) = 0;
+#pragma unroll 1
+  for (int r = 0; r < 10; r++) {
+    const XeReg R = reg_get(L, r);
+    mark_obj(L, int(XE_T_ALIAS(R.t)));
+    if (XE_ISPTR(R.t)) mark_handle(L, R.h);
+  }
+#pragma unroll 1
+  for (uint32_t e = 0; e < L.npres; e++)
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) {
+      const XeReg R = pres_get(L, e, r);
+      if (XE_ISPTR(R.t)) mark_handle(L, R.h);
+    }
+#pragma unroll 1
+  for (uint32_t f = 0; f <= L.npres && f < L.G->nframes; f++)
+#pragma unroll 1
+    for (int s = 0; s < XE_FRAME; s++) mark_obj(L, vmem_id(L, XeVR{int(f), XE_FRAME}, s));
+#pragma unroll 1
+  for (int s = 0; s < XE_CTX_LEN; s++) mark_obj(L, vmem_id(L, XeVR{8, XE_CTX_LEN}, s));
+  for (bool grew = true; grew;) {
+    grew = false;
+#pragma unroll 1
+    for (uint32_t k = 0; k < L.vnext; k++)
+      if (mark_get(L, vc_bit(L, k)))
+#pragma unroll 1
+        for (uint32_t s = 0; s < vc_len(L, k); s++) grew |= mark_obj(L, vmem_id(L, XeVR{16 + int(k), XE_FRAME}, s));
+#pragma unroll 1
+    for (uint32_t id = 1; id < L.onext; id++)
+      if (mark_get(L, id)) {
+        int64_t v; uint32_t h, t;
+        obj_get(L, int(id), v, h, t);
+        if (XE_ISPTR(t)) grew |= mark_handle(L, h);
+      }
+#pragma unroll 1
+    for (uint32_t k = 0; k < L.bnext; k++)
+      if (mark_get(L, bm_bit(L, k)) && *bm_field(L, k, XE_BM_MAT) == XE_NONE) grew |= mark_handle(L, *bm_field(L, k, XE_BM_SRC));
+  }
+  L.ofree = 0;
+#pragma unroll 1
+  for (uint32_t id = 1; id < L.onext; id++)
+    if (!mark_get(L, id)) *gat<uint32_t>(L, L.G->o_ofree, L.ofree++) = id;
+  L.vfree = 0;
+#pragma unroll 1
+  for (uint32_t k = 0; k < L.vnext; k++)
+    if (!mark_get(L, vc_bit(L, k))) *gat<uint32_t>(L, L.G->o_vfree, L.vfree++) = k;
+  L.bfree = 0;
+  bool any_bytes = false;
+#pragma unroll 1
+  for (uint32_t k = 0; k < L.bnext; k++) {
+    if (!mark_get(L, bm_bit(L, k))) {
+      if (*bm_field(L, k, XE_BM_MAT) == XE_NONE && *bm_field(L, k, XE_BM_SRC) != XE_NONE) L.npristine--;
+      *bm_field(L, k, XE_BM_SRC) = XE_NONE;  // a free record never matches a source
+      *bm_field(L, k, XE_BM_MAT) = 0;
+      *gat<uint32_t>(L, L.G->o_bfree, L.bfree++) = k;
+    } else if (*bm_field(L, k, XE_BM_MAT) != XE_NONE) {
+      any_bytes = true;
+    }
+  }
+  if (!any_bytes) L.bused = 0;
+}
+
+XE_DEV int obj_alloc(XeLane& L) {
+  if (L.ofree) return int(*gat<uint32_t>(L, L.G->o_ofree, --L.ofree));
+  if (L.onext < L.G->nobj) return int(L.onext++);
+  gen_gc(L);
+  if (L.ofree) return int(*gat<uint32_t>(L, L.G->o_ofree, --L.ofree));
+  return -1;
+}
+XE_DEV int vc_alloc(XeLane& L) {
+  if (L.vfree) return int(*gat<uint32_t>(L, L.G->o_vfree, --L.vfree));
+  if (L.vnext < L.G->nvc) return int(L.vnext++);
+  gen_gc(L);
+  if (L.vfree) return int(*gat<uint32_t>(L, L.G->o_vfree, --L.vfree));
+  return -1;
+}
+XE_DEV int bm_alloc(XeLane& L) {
+  if (L.bfree) return int(*gat<uint32_t>(L, L.G->o_bfree, --L.bfree));
+  if (L.bnext < L.G->nbm) return int(L.bnext++);
+  gen_gc(L);
+  if (L.bfree) return int(*gat<uint32_t>(L, L.G->o_bfree, --L.bfree));
+  return -1;
+}
+XE_DEV int64_t bytes_alloc(XeLane& L, uint64_t n) {
+  const uint64_t need = (n + 7) & ~uint64_t(7);
+  if (L.bused + need > L.G->nbytes) {
+    gen_gc(L);
+    if (L.bused + need > L.G->nbytes) return -1;
+  }
+  const uint64_t at = L.bused;
+  L.bused += need;
+  return int64_t(at);
+}
+#endif
 
 // ------------------------------------------------------------------ register writes
 XE_DEV void reg_replace(XeLane& L, int d, uint32_t kind, uint32_t h, int64_t v, uint32_t alias_and_ro) {
@@ -367,6 +616,7 @@ XE_DEV void alias_refresh(XeLane& L, uint32_t a, int64_t v) {
 // RegisterValue.Assign on register d's object (in place; registers.go:194-197,243-247,305-313)
 XE_DEV int reg_inplace(XeLane& L, int d, int64_t v, uint32_t cm = XE_CM_ALL) {
   XeReg r = reg_get(L, d);
+  XE_NILCHK(r);
   if (XE_T_KIND(r.t) == XE_KIND_FRAMEPTR && (r.t & XE_T_RO)) return XE_E_READONLY;
   r.v = v;
   reg_put(L, d, r);
@@ -432,12 +682,31 @@ XE_DEV void fp_record(XeLane& L, const XeParams& P, uint32_t m, bool atomic, uin
 struct XeBMem {
   uint8_t* base;
   int64_t len;
-  uint32_t map;     // 0 = packet
+  uint32_t map;     // map whose memory this is (footprints); 0 = the packet or a lane-private copy
   bool array;
 };
 
+// Map memories — and, in the general model, list / perf elements and lane-private ByteMemories (a
+// clone still reading through resolves to its source). The packet itself takes the header-window path.
 XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem& B) {
-  // map memories only (packet accesses take the header-window path)
+#if XE_GEN
+  while (xe_h_cls(h) == XE_H_BMEM) {
+    const uint32_t k = xe_h_slot(h);
+    const uint32_t mat = *bm_field(L, k, XE_BM_MAT);
+    if (mat != XE_NONE) {
+      B.base = (uint8_t*)(lane_bytes(L) + mat);
+      B.len = int64_t(*bm_field(L, k, XE_BM_LEN));
+      B.map = 0;
+      B.array = false;
+      return true;
+    }
+    h = *bm_field(L, k, XE_BM_SRC);
+  }
+  if (xe_h_cls(h) == XE_H_PKT) {
+    B.base = L.pkt; B.len = L.plen; B.map = 0; B.array = false;
+    return true;
+  }
+#endif
   uint32_t c = xe_h_cls(h);
   uint32_t m = xe_h_map(h);
   const XeDevMap M = map_desc(L, m);
@@ -445,12 +714,72 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   if (!XE_HAS_HASH || (XE_HAS_ARRAY && c == XE_H_ARRAY)) {
     B.base = M.vals; B.len = int64_t(M.vals_bytes); B.array = true; return true;
   }
+  B.array = false;
+#if XE_HAS_ORDERED
+  if (c == XE_H_QVAL) {
+    const uint64_t id = xe_h_slot(h);
+    if (M.kind == XE_DM_PERF) {
+      B.base = M.vals + ((XE_GP(const uint64_t))M.rec)[2 * id];
+      B.len = int64_t(((XE_GP(const uint64_t))M.rec)[2 * id + 1]);
+    } else {
+      B.base = M.vals + id * M.value_size;
+      B.len = int64_t(((XE_GP(const uint32_t))M.elen)[id]);
+    }
+    return true;
+  }
+  if (M.kind == XE_DM_LRU) {
+    const uint64_t vid = xe_h_slot(h);
+    B.base = M.vals + vid * M.value_size;
+    B.len = int64_t(((XE_GP(const uint32_t))M.elen)[vid]);
+    return true;
+  }
+#endif
   uint32_t slot = xe_h_slot(h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
   B.len = (uint32_t(((XE_GP(const uint64_t))M.keys)[uint64_t(slot) * M.rwords]) & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
-  B.array = false;
   return true;
 }
+
+#if XE_GEN
+// Give private ByteMemory k its own copy of the bytes it has been reading through to (its source as
+// it is now, which is what Registers.Clone copied at call time, registers.go:233-240: every write to
+// the source since then made this copy first). Taking a map's bytes while other lanes add to them is
+// order-dependent: parallel mode aborts to the ordered replay instead.
+XE_COLD int bm_materialize(XeLane& L, const XeParams& P, uint32_t k) {
+  const uint32_t n = *bm_field(L, k, XE_BM_LEN);
+  const int64_t at = bytes_alloc(L, n);
+  if (at < 0) return XE_EV_CAP;
+  if (*bm_field(L, k, XE_BM_SRC) == XE_NONE || *bm_field(L, k, XE_BM_MAT) != XE_NONE) return 0;  // collected meanwhile
+  XeBMem S;
+  bmem_resolve(L, P, *bm_field(L, k, XE_BM_SRC), S);
+  if (P.mode == XE_MODE_PARALLEL && S.map) return XE_EV_ORD;
+  XE_GP(uint8_t) d = lane_bytes(L) + at;
+#pragma unroll 1
+  for (uint32_t i = 0; i < n; i++) d[i] = ((XE_GP(const uint8_t))S.base)[i];
+  *bm_field(L, k, XE_BM_MAT) = uint32_t(at);
+  L.npristine--;
+  return 0;
+}
+// Before this lane writes the ByteMemory identified by `ident`, every private copy still reading
+// through to it takes its bytes.
+XE_DEV int bm_before_write(XeLane& L, const XeParams& P, uint32_t ident) {
+  if (!L.npristine) return 0;
+#pragma unroll 1
+  for (uint32_t k = 0; k < L.bnext; k++) {
+    if (*bm_field(L, k, XE_BM_MAT) != XE_NONE || *bm_field(L, k, XE_BM_SRC) != ident) continue;
+    if (int e = bm_materialize(L, P, k)) return e;
+  }
+  return 0;
+}
+XE_DEV uint32_t bm_ident(uint32_t h) { return xe_h_cls(h) == XE_H_ARRAY ? xe_h_make(XE_H_ARRAY, xe_h_map(h), 0) : h; }
+// a write through handle h: its readers-through copy first; a private ByteMemory still reading
+// through to its source gets its own bytes
+XE_DEV int bm_prepare_write(XeLane& L, const XeParams& P, uint32_t h) {
+  if (int e = bm_before_write(L, P, bm_ident(h))) return e;
+  if (xe_h_cls(h) == XE_H_BMEM && *bm_field(L, xe_h_slot(h), XE_BM_MAT) == XE_NONE) return bm_materialize(L, P, xe_h_slot(h));
+  return 0;
+}
+#endif
 
 // Go bounds check with wrapping add; passing the check with off >= len (overflow) panics at the index
 XE_DEV int bounds(int64_t off, int64_t size, int64_t len) {
@@ -665,43 +994,19 @@ XE_DEV void acc_flush(const XeLane& L) {
 }
 
 // ------------------------------------------------------------------ ValueMemory access
-// region words: stack frame 0 = words 0..31 (len 256), ctx = words 32..34 (len 24)
-XE_DEV void vmem_region(uint32_t h, int& wb, int64_t& len) {
-  if (xe_h_cls(h) == XE_H_CTX) { wb = XE_CTX_WORD0; len = XE_CTX_LEN; }
-  else { wb = 0; len = 256; }
-}
-
-XE_DEV int vmem_byte(const XeLane& L, int wb, int64_t off) {
-  uint64_t word = bm_word(L, wb + int(off >> 3));
-  return int((word >> (8 * (off & 7))) & 0xffu);
-}
+XE_DEV bool is_vm_cls(uint32_t c) { return c == XE_H_CTX || c == XE_H_STACK || (XE_GEN && c == XE_H_VCLONE); }
 
 // ValueMemory.Read, memory.go:32-53 -> object id
 XE_DEV int vmem_read(const XeLane& L, uint32_t h, int64_t off, int size, int& id) {
-  int wb; int64_t len;
-  vmem_region(h, wb, len);
-  if (int e = bounds(off, size, len)) return e;
-  int first = vmem_byte(L, wb, off);
+  const XeVR R = vmem_region(L, h);
+  if (int e = bounds(off, size, R.len)) return e;
+  int first = vmem_id(L, R, off);
   XE_UNROLL_VM
   for (int i = 1; i < size; i++)
-    if (vmem_byte(L, wb, off + i) != first) return XE_E_NONCONTIG;
+    if (vmem_id(L, R, off + i) != first) return XE_E_NONCONTIG;
   if (!first) return XE_E_UNINIT;
   id = first;
   return 0;
-}
-
-XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
-  int64_t end = off + size;
-  int w0 = int(off >> 3), w1 = int((end - 1) >> 3);
-  XE_UNROLL_VM
-  for (int w = w0; w <= w1; w++) {
-    int64_t lo = off > int64_t(w) * 8 ? off - int64_t(w) * 8 : 0;
-    int64_t hi = end < int64_t(w + 1) * 8 ? end - int64_t(w) * 8 : 8;
-    uint64_t mask = (hi - lo == 8) ? ~0ull : (((1ull << (8 * (hi - lo))) - 1ull) << (8 * lo));
-    uint64_t word = bm_word(L, wb + w);
-    word = (word & ~mask) | ((uint64_t(id) * 0x0101010101010101ull) & mask);
-    bm_set_word(L, wb + w, word);
-  }
 }
 
 // ------------------------------------------------------------------ generic memory ops
@@ -709,7 +1014,7 @@ XE_DEV void vmem_fill(XeLane& L, int wb, int64_t off, int size, int id) {
 XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size, bool track,
                     uint32_t& kind, uint32_t& oh, int64_t& val, uint32_t& alias, uint32_t cm = XE_CM_ALL) {
   uint32_t c = xe_h_cls(h);
-  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
+  if ((cm & XE_CM_VM) && is_vm_cls(c)) {
     int id = 0;
     if (int e = vmem_read(L, h, off, size, id)) return e;
     uint32_t t;
@@ -730,7 +1035,7 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (track) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, size));
+  if (track && B.map) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, size));
   val = int64_t(load_le(B.base + off, size));
   kind = XE_KIND_IMM;
   oh = 0;
@@ -742,18 +1047,20 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
 XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int size,
                      uint32_t kind, uint32_t oh, int64_t val, uint32_t cm = XE_CM_ALL) {
   uint32_t c = xe_h_cls(h);
-  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
-    int wb; int64_t len;
-    vmem_region(h, wb, len);
-    if (int e = bounds(off, size, len)) return e;
+  if ((cm & XE_CM_VM) && is_vm_cls(c)) {
+    const XeVR R = vmem_region(L, h);
+    if (int e = bounds(off, size, R.len)) return e;
     int id = obj_alloc(L);
     if (id < 0) return XE_EV_CAP;
     obj_set(L, id, val, oh, kind);
-    vmem_fill(L, wb, off, size, id);
+    vmem_fill(L, R, off, size, id);
     return 0;
   }
   if ((cm & XE_CM_PKT) && c == XE_H_PKT) {
     if (int e = bounds(off, size, L.plen)) return e;
+#if XE_GEN
+    if (int e = bm_before_write(L, P, h)) return e;
+#endif
     pkt_store(L, off, size, uint64_t(val));
     return 0;
   }
@@ -761,25 +1068,28 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // non-commutative shared write
+  if (P.mode == XE_MODE_PARALLEL && B.map) return XE_EV_ORD;  // non-commutative shared write
+#if XE_GEN
+  if (int e = bm_prepare_write(L, P, h)) return e;
+  bmem_resolve(L, P, h, B);
+#endif
   store_le(B.base + off, size, uint64_t(val));
   return 0;
 }
 
 // PointerValue.ReadRange (registers.go:218-220,273-281; memory.go:55-95,176-185).
-// emit(i, byte) receives the output bytes. Returns 0 / XE_E_OOB / panic. dry = validate only.
+// emit(i, byte) receives the output bytes. Returns 0 / XE_E_OOB / panic.
 template <class Emit>
-XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Emit emit, uint32_t cm = XE_CM_ALL) {
-  const XeReg R = reg_get(L, r);
+XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, const XeReg& R, int64_t count, Emit emit, uint32_t cm = XE_CM_ALL) {
   uint32_t kind = XE_T_KIND(R.t);
   uint32_t h = R.h;
-  int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R.v) : R.v;
+  int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, R.v) : R.v;
   uint32_t c = xe_h_cls(h);
-  if ((cm & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
-    int wb; int64_t len;
-    vmem_region(h, wb, len);
-    if (off < 0 || xe_wadd(off, count) > len) return XE_E_OOB;
-    if (off >= len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
+  if ((cm & XE_CM_VM) && is_vm_cls(c)) {
+    const XeVR Rg = vmem_region(L, h);
+    if (off < 0 || xe_wadd(off, count) > Rg.len) return XE_E_OOB;
+    if (count < 0) return XE_EV_PANIC | XE_P_MAKESLICE;
+    if (off >= Rg.len && count > 0) return XE_EV_PANIC | XE_P_INDEX;
     // Byte groups of equal object references, each written 1/2/4/8 bytes wide (memory.go:61-91).
     // Written as fixed-trip loops (skip counts the bytes a wide write already produced) so that a
     // per-program kernel with a constant count unrolls it fully and folds the object ids.
@@ -787,13 +1097,13 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
     XE_UNROLL_VM
     for (int64_t i = 0; i < count; i++) {
       if (skip > 0) { skip--; continue; }
-      const int v = vmem_byte(L, wb, off + i);
+      const int v = vmem_id(L, Rg, off + i);
       if (!v) { emit(i, 0); continue; }
       int size = 1;
       bool run = true;
       XE_UNROLL_VM
       for (int j = 1; j < 8; j++) {
-        run = run && i + j < count && vmem_byte(L, wb, off + i + j) == v;
+        run = run && i + j < count && vmem_id(L, Rg, off + i + j) == v;
         size += run ? 1 : 0;
       }
       const int w = size > 4 ? 8 : size > 2 ? 4 : size > 1 ? 2 : 1;
@@ -809,6 +1119,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
   }
   if ((cm & XE_CM_PKT) && c == XE_H_PKT) {
     if (off < 0 || xe_wadd(off, count) > L.plen) return XE_E_OOB;
+    if (count < 0) return XE_EV_PANIC | XE_P_MAKESLICE;
 #pragma unroll 1
     for (int64_t i = 0; i < count; i++) emit(i, uint8_t(pkt_load(L, off + i, 1)));
     return 0;
@@ -817,22 +1128,22 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, int r, int64_t count, Em
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
-  if (count > 0) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, int(count)));
+  if (count < 0) return XE_EV_PANIC | XE_P_MAKESLICE;
+  if (count > 0 && B.map) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, int(count)));
 #pragma unroll 1
   for (int64_t i = 0; i < count; i++) emit(i, ((XE_GP(const uint8_t))B.base)[off + i]);
   return 0;
 }
 
 // ------------------------------------------------------------------ hash map
-XE_DEV uint32_t hash_state(const XeDevMap& M, uint64_t slot) {
-  return uint32_t(((XE_GP(const uint64_t))M.keys)[slot * M.rwords]);
-}
+XE_DEV uint64_t hash_word0(const XeDevMap& M, uint64_t slot) { return ((XE_GP(const uint64_t))M.keys)[slot * M.rwords]; }
+XE_DEV uint32_t hash_state(const XeDevMap& M, uint64_t slot) { return uint32_t(hash_word0(M, slot)); }
 XE_DEV void hash_set_state(const XeDevMap& M, uint64_t slot, uint32_t st) {
-  ((XE_GP(uint64_t))M.keys)[slot * M.rwords] = st;
+  ((XE_GP(uint64_t))M.keys)[slot * M.rwords] = (hash_word0(M, slot) & ~0xffffffffull) | st;
 }
 
 // Linear probing over slot records: the state word and the key words of a record are loaded
-// together (independent loads of one line), then compared.
+// together (independent loads of one line), then compared. LRU maps leave tombstones behind evictions.
 XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
   if (empty) return (hash_state(M, M.cap) & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
@@ -845,7 +1156,12 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
 #pragma unroll
     for (uint32_t k = 0; k <= XE_MAX_KEY / 8; k++)
       if (k <= M.kwords) w[k] = r[k];
-    if (!(uint32_t(w[0]) & XE_SLOT_FULL)) return -1;
+    const uint32_t st = uint32_t(w[0]);
+    if (!(st & XE_SLOT_FULL)) {
+      if (!XE_HAS_ORDERED || !(st & XE_SLOT_TOMB)) return -1;
+      idx = (idx + 1) & mask;
+      continue;
+    }
     bool eq = true;
 #pragma unroll
     for (uint32_t k = 0; k < XE_MAX_KEY / 8; k++)
@@ -856,11 +1172,11 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
   return -1;
 }
 
-// insert a new key (sequential mode only); returns slot
+// insert a new key (sequential mode only); returns slot (LRU: the first free or tombstone slot)
 XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty) {
   if (empty) {
     hash_set_state(M, M.cap, XE_SLOT_FULL);
-    *M.count += 1;
+    if (M.kind == XE_DM_HASH) *M.count += 1;
     return int64_t(M.cap);
   }
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
@@ -870,16 +1186,16 @@ XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty
   uint64_t* k = M.keys + uint64_t(idx) * M.rwords + 1;
   for (uint32_t w = 0; w < M.kwords; w++) k[w] = kw[w];
   hash_set_state(M, idx, XE_SLOT_FULL);
-  *M.count += 1;
+  if (M.kind == XE_DM_HASH) *M.count += 1;
   return int64_t(idx);
 }
 
 // read a key through a pointer register into zero-padded words; ReadRange errors give the nil key
 // (maps_hash.go:50-53). Returns a panic code or 0.
-XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint64_t* kw, bool& empty,
+XE_DEV int read_key(XeLane& L, const XeParams& P, const XeReg& R, const XeDevMap& M, uint64_t* kw, bool& empty,
                     uint32_t cm = XE_CM_ALL) {
   for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
-  int e = ptr_read_range(L, P, r, int64_t(M.key_size), [&](int64_t i, uint8_t b) {
+  int e = ptr_read_range(L, P, R, int64_t(M.key_size), [&](int64_t i, uint8_t b) {
     kw[i >> 3] |= uint64_t(b) << (8 * (i & 7));
   }, cm);
   if (XE_IS_PANIC(e)) return e;
@@ -889,10 +1205,77 @@ XE_DEV int read_key(XeLane& L, const XeParams& P, int r, const XeDevMap& M, uint
   return 0;
 }
 
+// The key bytes bpf_map_peek_elem hands to Lookup: ReadRange of a 4-slot ValueMemory holding one IMM 0
+// (helper_functions.go:345-355): > 4 bytes is out of range (nil key), 3 bytes widen to 4 and panic.
+XE_DEV int peek_key(const XeDevMap& M, uint64_t* kw, bool& empty) {
+  for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
+  empty = M.key_size > 4 || M.key_size == 0;
+  if (M.key_size == 3) return XE_EV_PANIC | XE_P_INDEX;
+  return 0;
+}
+
+#if XE_HAS_ORDERED
+// ---- LRU_HASH (emulator/maps_hash_lru.go): value ids index the value pool; the UsageList is a doubly
+// linked list over them (head = most recently used). link[4 v] = prev, [4 v + 1] = next, [4 v + 2] = slot.
+XE_DEV XE_GP(uint32_t) lru_link(const XeDevMap& M, uint32_t v, int f) { return (XE_GP(uint32_t))M.link + 4 * uint64_t(v) + f; }
+XE_DEV XE_GP(uint64_t) map_hdr(const XeDevMap& M, int w) { return (XE_GP(uint64_t))M.hdr + w; }
+XE_DEV void lru_unlink(const XeDevMap& M, uint32_t v) {
+  const uint32_t p = *lru_link(M, v, 0), n = *lru_link(M, v, 1);
+  if (p != XE_NONE) *lru_link(M, p, 1) = n; else *map_hdr(M, 0) = n;
+  if (n != XE_NONE) *lru_link(M, n, 0) = p; else *map_hdr(M, 1) = p;
+}
+XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
+  const uint32_t h = uint32_t(*map_hdr(M, 0));
+  *lru_link(M, v, 0) = XE_NONE;
+  *lru_link(M, v, 1) = h;
+  if (h != XE_NONE) *lru_link(M, h, 0) = v; else *map_hdr(M, 1) = v;
+  *map_hdr(M, 0) = v;
+}
+XE_DEV void lru_promote(const XeDevMap& M, uint32_t v) {  // promote, :51-68
+  if (uint32_t(*map_hdr(M, 0)) == v) return;
+  lru_unlink(M, v);
+  lru_push_front(M, v);
+}
+XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_word0(M, uint64_t(slot)) >> 32); }
+// LRU lookup of a key (no promotion); value id or XE_NONE
+XE_DEV uint32_t lru_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
+  const int64_t s = hash_find(M, kw, empty);
+  return s < 0 ? XE_NONE : lru_vid(M, s);
+}
+// delete, :163-183 (evicted values keep their pool entry: pointers to them stay valid)
+XE_DEV void lru_erase(const XeDevMap& M, uint32_t v) {
+  const uint32_t slot = *lru_link(M, v, 2);
+  ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_TOMB;
+  lru_unlink(M, v);
+  *map_hdr(M, 2) -= 1;
+}
+XE_DEV int lru_insert(const XeDevMap& M, const uint64_t* kw, bool empty, uint32_t& v) {
+  const uint64_t nv = *map_hdr(M, 3);
+  if (nv >= M.pool_cap) return XE_EV_CAP;
+  v = uint32_t(nv);
+  *map_hdr(M, 3) = nv + 1;
+  const int64_t slot = hash_insert_new(M, kw, empty);
+  ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_FULL | (uint64_t(v) << 32);
+  *lru_link(M, v, 2) = uint32_t(slot);
+  ((XE_GP(uint32_t))M.elen)[v] = M.value_size;
+  *map_hdr(M, 2) += 1;
+  lru_push_front(M, v);  // appended to the UsageList, then promoted to its top (:144-150)
+  return 0;
+}
+
+// ---- QUEUE / STACK (emulator/maps_queue.go, maps_stack.go): element ids index the element pool;
+// link holds the list (a ring of list_cap ids for a queue). hdr = {head, count, next id, -, is_stack}
+XE_DEV uint32_t list_at(const XeDevMap& M, uint64_t i) {  // Values[i] in Go slice order
+  const uint64_t head = *map_hdr(M, 0);
+  return ((XE_GP(const uint32_t))M.link)[*map_hdr(M, 4) ? i : (head + i) % M.list_cap];
+}
+#endif
+
 // ------------------------------------------------------------------ helpers
 // regToMap, helper_functions.go:109-130. m = 0 means "R0 := 0, helper returns nil".
 XE_DEV int reg_to_map(XeLane& L, const XeParams& P, uint32_t& m, uint32_t cm1 = XE_CM_ALL) {
   const XeReg R1 = reg_get(L, 1);
+  XE_NILCHK(R1);
   int64_t idx = R1.v;
   if ((cm1 & ~(XE_CM_IMM | XE_CM_ALIAS)) && XE_T_KIND(R1.t) == XE_KIND_MEMPTR) {
     uint32_t k, oh, al; int64_t v;
@@ -912,90 +1295,249 @@ XE_DEV int helper_errno_result(XeLane& L, int64_t v) {
   reg_replace(L, 0, XE_KIND_IMM, 0, v, 0);
   return 0;
 }
+XE_DEV int in_helper(int e) { return (e & 0xf000) ? e : (e | XE_E_IN_HELPER); }
+
+// Map.Lookup of map m for `key` (a register value: pointer or not). Sets out (the RegisterValue
+// Lookup returns) or returns errno via *errno_out (sentinel errors), a VM error or a panic.
+// ArrayMap.Lookup maps_array.go:65-87, HashMap.Lookup maps_hash.go:44-63, HashMapLRU.Lookup
+// maps_hash_lru.go:70-91, QueueMap/StackMap.Lookup maps_queue.go:39-58 / maps_stack.go:38-58,
+// PerfEventArray.Lookup maps_perf_event_array.go:45-65. `peek`: the key is bpf_map_peek_elem's IMM 0.
+XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, bool peek, XeReg& out, int64_t& err,
+                      uint32_t cm2 = XE_CM_ALL) {
+  const XeDevMap M = map_desc(L, m);
+  err = 0;
+  out = XeReg{0, 0, XE_KIND_IMM};
+  if (!peek && !XE_ISPTR(K.t)) { err = -14; return 0; }  // errMapKeyNoPtr
+  if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {
+    int64_t kv = 0;
+    if (!peek) {
+      uint32_t kind = XE_T_KIND(K.t);
+      int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, K.v) : K.v;
+      uint32_t k, oh, al;
+      int e = mem_read(L, P, K.h, off, 4, true, k, oh, kv, al, cm2);
+      if (XE_IS_PANIC(e)) return e;
+      if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;  // error ignored, nil keyValReg.Value()
+    }
+    int64_t voff = xe_wmul(kv, int64_t(M.value_size));
+    if (voff < int64_t(M.vals_bytes)) out = XeReg{voff, xe_h_make(XE_H_ARRAY, m, 0), XE_KIND_MEMPTR};
+    return 0;
+  }
+  if ((XE_HAS_HASH && M.kind == XE_DM_HASH) || (XE_HAS_ORDERED && M.kind == XE_DM_LRU)) {
+    uint64_t kw[XE_MAX_KEY / 8];
+    bool empty = false;
+    if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2)) return e;
+#if XE_HAS_ORDERED
+    if (M.kind == XE_DM_LRU) {
+      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // a lookup promotes: a write to the UsageList
+      const uint32_t v = lru_find(M, kw, empty);
+      if (v == XE_NONE) return 0;
+      lru_promote(M, v);
+      out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
+      return 0;
+    }
+#endif
+    int64_t slot = hash_find(M, kw, empty);
+    if (slot >= 0) out = XeReg{0, xe_h_make(XE_H_HASH, m, uint32_t(slot)), XE_KIND_MEMPTR};
+    return 0;
+  }
+#if XE_HAS_ORDERED
+  if (M.kind == XE_DM_LIST || M.kind == XE_DM_PERF) {
+    if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // the list changes in packet order
+    int64_t kv = 0;
+    if (!peek) {
+      int64_t off = XE_T_KIND(K.t) == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, K.v) : K.v;
+      uint32_t k, oh, al;
+      int e = mem_read(L, P, K.h, off, 4, true, k, oh, kv, al, cm2);
+      if (XE_IS_PANIC(e)) return e;
+      if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;
+    }
+    if (M.kind == XE_DM_PERF) {
+      const int64_t cnt = int64_t(*map_hdr(M, 0));
+      if (kv >= cnt) return 0;
+      if (kv < 0) return XE_EV_PANIC | XE_P_INDEX;
+      out = XeReg{0, xe_h_make(XE_H_QVAL, m, uint32_t(kv)), XE_KIND_MEMPTR};
+      return 0;
+    }
+    const int64_t cnt = int64_t(*map_hdr(M, 1));
+    if (kv < 0 || kv >= cnt) { err = -7; return 0; }  // errMapOutOfMemory
+    const uint32_t id = list_at(M, uint64_t(*map_hdr(M, 4) ? cnt - 1 - kv : kv));
+    out = XeReg{0, xe_h_make(XE_H_QVAL, m, id), XE_KIND_MEMPTR};
+    return 0;
+  }
+#endif
+  return XE_EV_UNSUP;
+}
 
 // MapLookupElement, helper_functions.go:46-73
 XE_DEV int helper_lookup(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL) {
   uint32_t m;
-  if (int e = reg_to_map(L, P, m, cm1)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
   if (!m) return 0;
-  const XeDevMap M = map_desc(L, m);
-  const XeReg R2 = reg_get(L, 2);
-  if (XE_T_KIND(R2.t) == XE_KIND_IMM) return helper_errno_result(L, -14);  // errMapKeyNoPtr
-  if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Lookup, maps_array.go:65-87
-    uint32_t kind = XE_T_KIND(R2.t);
-    int64_t off = kind == XE_KIND_FRAMEPTR ? xe_wadd(256, R2.v) : R2.v;
-    uint32_t k, oh, al; int64_t kv;
-    int e = mem_read(L, P, R2.h, off, 4, true, k, oh, kv, al, cm2);
-    if (XE_IS_PANIC(e)) return e;
-    if (e) return XE_EV_PANIC | XE_P_NIL_DEREF;  // error ignored, nil keyValReg.Value()
-    int64_t voff = xe_wmul(kv, int64_t(M.value_size));
-    if (voff >= int64_t(M.vals_bytes)) reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
-    else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_ARRAY, m, 0), voff, 0);
-    return 0;
-  }
-  if (XE_HAS_HASH && M.kind == XE_DM_HASH) {  // HashMap.Lookup, maps_hash.go:44-63
-    uint64_t kw[XE_MAX_KEY / 8];
-    bool empty = false;
-    if (int e = read_key(L, P, 2, M, kw, empty, cm2)) return e;
-    int64_t slot = hash_find(M, kw, empty);
-    if (slot < 0) reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
-    else reg_replace(L, 0, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), 0, 0);
-    return 0;
-  }
-  return XE_EV_UNSUP;
+  XeReg out;
+  int64_t err;
+  if (int e = map_lookup(L, P, m, reg_get(L, 2), false, out, err, cm2)) return in_helper(e);
+  if (err) return helper_errno_result(L, err);
+  reg_put(L, 0, out);
+  return 0;
+}
+
+// ReadRange(0, n) of register R into the bytes at dst (a map value / pool element). Returns 0, a
+// panic, or 1 when the range could not be read (the Go code ignores that error and stores a nil backing).
+XE_DEV int read_value_into(XeLane& L, const XeParams& P, const XeReg& R, int64_t n, uint8_t* dst, uint32_t cm = XE_CM_ALL) {
+  int ve = ptr_read_range(L, P, R, n, [&](int64_t, uint8_t) {}, cm);  // validate first: a panic leaves dst untouched
+  if (XE_IS_PANIC(ve)) return ve;
+  if (ve) return 1;
+  ptr_read_range(L, P, R, n, [&](int64_t i, uint8_t b) { ((XE_GP(uint8_t))dst)[i] = b; }, cm);
+  return 0;
 }
 
 // MapUpdateElement, helper_functions.go:76-101
 XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
                          uint32_t cm3 = XE_CM_ALL) {
   uint32_t m;
-  if (int e = reg_to_map(L, P, m, cm1)) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+  if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
   if (!m) return 0;
+  XE_NILCHK(reg_get(L, 4));  // BPFAttrMapElemFlags(R4.Value())
   const XeDevMap M = map_desc(L, m);
+  const XeReg R2 = reg_get(L, 2), R3 = reg_get(L, 3);
   if (XE_HAS_ARRAY && M.kind == XE_DM_ARRAY) {  // ArrayMap.Update, maps_array.go:89-131
-    const XeReg R2 = reg_get(L, 2), R3 = reg_get(L, 3);
     if (XE_T_KIND(R3.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     if (XE_T_KIND(R2.t) != XE_KIND_MEMPTR) return helper_errno_result(L, -14);
     uint32_t k, oh, al; int64_t kv;
-    if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al, cm2))
-      return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+    if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al, cm2)) return in_helper(e);
     if (kv >= int64_t(M.vals_bytes)) return helper_errno_result(L, -7);
 #pragma unroll 1
     for (int64_t i = 0; i < int64_t(M.value_size); i++) {
       int64_t v;
-      if (int e = mem_read(L, P, R3.h, i, 1, true, k, oh, v, al, cm3))  // ignores the value ptr offset
-        return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+      if (int e = mem_read(L, P, R3.h, i, 1, true, k, oh, v, al, cm3)) return in_helper(e);  // ignores the value ptr offset
       int64_t dst = xe_wadd(xe_wmul(kv, int64_t(M.value_size)), i);
-      if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return (e & 0xf000) ? e : (e | XE_E_IN_HELPER);
+      if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return in_helper(e);
       if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+#if XE_GEN
+      if (int e = bm_before_write(L, P, xe_h_make(XE_H_ARRAY, m, 0))) return e;
+#endif
       M.vals[dst] = uint8_t(v);
     }
     return helper_errno_result(L, 0);
   }
   if (XE_HAS_HASH && M.kind == XE_DM_HASH) {  // HashMap.Update, maps_hash.go:65-123
-    if (XE_T_KIND(reg_get(L, 2).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    if (!XE_ISPTR(R2.t)) return helper_errno_result(L, -14);
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = read_key(L, P, 2, M, kw, empty, cm2)) return e;
+    if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
     int64_t slot = hash_find(M, kw, empty);
     if (slot < 0 && uint64_t(*M.count) + 1 > M.max_entries) return helper_errno_result(L, -7);
-    if (XE_T_KIND(reg_get(L, 3).t) == XE_KIND_IMM) return helper_errno_result(L, -14);
+    if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
     // value ReadRange: validate first (a panic must leave the map untouched)
-    int ve = ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
+    int ve = ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
     if (XE_IS_PANIC(ve)) return ve;
     if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
     if (slot < 0) slot = hash_insert_new(M, kw, empty);
+#if XE_GEN
+    if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, uint32_t(slot)))) return e;
+#endif
     uint8_t* dst = M.vals + uint64_t(slot) * M.value_size;
     if (ve) {
       hash_set_state(M, uint64_t(slot), hash_state(M, uint64_t(slot)) | XE_SLOT_VLEN0);  // nil backing
     } else {
       hash_set_state(M, uint64_t(slot), hash_state(M, uint64_t(slot)) & ~XE_SLOT_VLEN0);
-      ptr_read_range(L, P, 3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; }, cm3);
+      ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { dst[i] = b; }, cm3);
     }
     return helper_errno_result(L, 0);
   }
+#if XE_HAS_ORDERED
+  if (M.kind == XE_DM_LRU) {  // HashMapLRU.Update, maps_hash_lru.go:93-161
+    if (!XE_ISPTR(R2.t)) return helper_errno_result(L, -14);
+    if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+    uint64_t kw[XE_MAX_KEY / 8];
+    bool empty = false;
+    if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
+    uint32_t v = lru_find(M, kw, empty);
+    if (v == XE_NONE && *map_hdr(M, 2) + 1 > M.max_entries) {
+      const uint32_t tail = uint32_t(*map_hdr(M, 1));
+      if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
+      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, tail))) return e;
+      lru_erase(M, tail);  // evicted before the value is checked
+    }
+    if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
+    int ve = ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
+    if (XE_IS_PANIC(ve)) return ve;
+    if (v == XE_NONE) {
+      if (int e = lru_insert(M, kw, empty, v)) return e;
+    } else {
+      lru_promote(M, v);
+      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
+    }
+    uint8_t* dst = M.vals + uint64_t(v) * M.value_size;
+    ((XE_GP(uint32_t))M.elen)[v] = ve ? 0u : M.value_size;
+    if (!ve) ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { ((XE_GP(uint8_t))dst)[i] = b; }, cm3);
+    return helper_errno_result(L, 0);
+  }
+  if (M.kind == XE_DM_PERF) return helper_errno_result(L, -1);  // errMapNotImplemented -> eperm
+  if (M.kind == XE_DM_LIST) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "update not available on this map type"
+#endif
   return XE_EV_UNSUP;
 }
+
+#if XE_HAS_ORDERED
+// QueueMap/StackMap.Push (maps_queue.go:60-77) and PerfEventArray.Push (maps_perf_event_array.go:101-115):
+// append ReadRange(0, size) of register R (nil backing when the range cannot be read)
+XE_COLD int list_push(XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, const XeReg& R, int64_t size, int64_t& err) {
+  err = 0;
+  if (!XE_ISPTR(R.t)) { err = -14; return 0; }  // errMapValNoPtr / errMapKeyNoPtr
+  if (M.kind == XE_DM_PERF) {
+    const uint64_t c = *map_hdr(M, 0), used = *map_hdr(M, 1);
+    int ve = ptr_read_range(L, P, R, size, [&](int64_t, uint8_t) {});
+    if (XE_IS_PANIC(ve)) return ve;
+    const uint64_t n = ve ? 0 : uint64_t(size);
+    if (c >= M.pool_cap || used + n > M.data_cap) return XE_EV_CAP;
+    if (n) ptr_read_range(L, P, R, size, [&](int64_t i, uint8_t b) { ((XE_GP(uint8_t))M.vals)[used + uint64_t(i)] = b; });
+    ((XE_GP(uint64_t))M.rec)[2 * c] = used;
+    ((XE_GP(uint64_t))M.rec)[2 * c + 1] = n;
+    *map_hdr(M, 0) = c + 1;
+    *map_hdr(M, 1) = used + ((n + 7) & ~uint64_t(7));
+    return 0;
+  }
+  const uint64_t id = *map_hdr(M, 2), cnt = *map_hdr(M, 1);
+  if (id >= M.pool_cap || cnt >= M.list_cap) return XE_EV_CAP;
+  uint8_t* dst = M.vals + id * M.value_size;
+  int e = read_value_into(L, P, R, size, dst);
+  if (XE_IS_PANIC(e)) return e;
+  ((XE_GP(uint32_t))M.elen)[id] = e ? 0u : uint32_t(size);
+  *map_hdr(M, 2) = id + 1;
+  const uint64_t at = *map_hdr(M, 4) ? cnt : (*map_hdr(M, 0) + cnt) % M.list_cap;
+  ((XE_GP(uint32_t))M.link)[at] = uint32_t(id);
+  *map_hdr(M, 1) = cnt + 1;
+  return 0;
+}
+
+// TailCall, helper_functions.go:133-210. Returns XE_EV_JUMP on success (PI switched, PC := -1).
+#define XE_EV_JUMP 0x5000
+XE_COLD int helper_tail_call(XeLane& L, const XeParams& P) {
+#if XE_GEN
+  const XeReg R2 = reg_get(L, 2);
+  XE_NILCHK(R2);
+  if (R2.v < 1 || R2.v > int64_t(P.nmaps)) return helper_errno_result(L, -14);
+  const uint32_t m = uint32_t(R2.v);
+  const XeDevMap M = map_desc(L, m);
+  if (M.btype != XE_MAP_PROG_ARRAY) return helper_errno_result(L, -14);
+  // key: a ValueMemory of 4 slots all holding the R3 object itself: Deref(0, W) returns it
+  const XeReg R3 = reg_get(L, 3);
+  XE_NILCHK(R3);
+  const int64_t off = xe_wmul(R3.v, int64_t(M.value_size));
+  if (off >= int64_t(M.vals_bytes)) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "lookup didn't return a pointer"
+  uint32_t k, oh, al; int64_t prog;
+  if (int e = mem_read(L, P, xe_h_make(XE_H_ARRAY, m, 0), off, 4, true, k, oh, prog, al)) return in_helper(e);
+  if (int64_t(P.nprogs) + 1 < prog) return helper_errno_result(L, -14);  // len(vm.Programs) < progIdx
+  if (prog == 0) return XE_E_NO_PROGRAM | XE_E_IN_HELPER;
+  L.pi = int32_t(prog);
+  reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
+  return XE_EV_JUMP;
+#else
+  return XE_EV_UNSUP;
+#endif
+}
+#endif
 
 XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
                        uint32_t cm3 = XE_CM_ALL) {
@@ -1006,7 +1548,77 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
     case 2: return helper_update(L, P, cm1, cm2, cm3);
     case 3: return XE_E_NOT_IMPL | XE_E_IN_HELPER;
     case 14: reg_replace(L, 0, XE_KIND_IMM, 0, (int64_t(1234) << 32) + 5678, 0); return 0;
+#if XE_HAS_ORDERED
+    case 12: return helper_tail_call(L, P);
+    case 25: {  // PerfEventOutput :219-252: R2 = map index (no deref), R4 = data, R5 = size
+      const XeReg R2 = reg_get(L, 2);
+      XE_NILCHK(R2);
+      if (R2.v < 1 || R2.v > int64_t(P.nmaps)) return helper_errno_result(L, -14);
+      const uint32_t m = uint32_t(R2.v);
+      const XeDevMap M = map_desc(L, m);
+      if (M.kind != XE_DM_PERF) return helper_errno_result(L, -14);
+      const XeReg R5 = reg_get(L, 5);
+      XE_NILCHK(R5);
+      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // events are appended in packet order
+      int64_t err;
+      if (int e = list_push(L, P, m, M, reg_get(L, 4), R5.v, err)) return in_helper(e);
+      return helper_errno_result(L, err);
+    }
+    case 87: {  // MapPushElement :255-281
+      uint32_t m;
+      if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
+      if (!m) return 0;
+      const XeDevMap M = map_desc(L, m);
+      if (M.kind != XE_DM_LIST && M.kind != XE_DM_PERF) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "push not available"
+      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+      int64_t err;
+      if (int e = list_push(L, P, m, M, reg_get(L, 2), int64_t(M.value_size), err)) return in_helper(e);
+      return helper_errno_result(L, err);
+    }
+    case 88: {  // MapPopElement :284-332
+      uint32_t m;
+      if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
+      if (!m) return 0;
+      reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
+      const XeDevMap M = map_desc(L, m);
+      if (M.kind != XE_DM_LIST) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "pop not available"
+      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+      XeReg val{0, 0, XE_KIND_IMM};
+      const uint64_t cnt = *map_hdr(M, 1);
+      if (cnt) {
+        uint32_t id;
+        if (*map_hdr(M, 4)) {
+          id = list_at(M, cnt - 1);
+        } else {
+          id = list_at(M, 0);
+          *map_hdr(M, 0) = (*map_hdr(M, 0) + 1) % M.list_cap;
+        }
+        *map_hdr(M, 1) = cnt - 1;
+        val = XeReg{0, xe_h_make(XE_H_QVAL, m, id), XE_KIND_MEMPTR};
+      }
+      const XeReg R2 = reg_get(L, 2);
+      if (XE_T_KIND(R2.t) == XE_KIND_MEMPTR || XE_T_KIND(R2.t) == XE_KIND_FRAMEPTR) {
+        const int64_t off = XE_T_KIND(R2.t) == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, R2.v) : R2.v;
+        if (int e = mem_write(L, P, R2.h, off, 8, XE_T_KIND(val.t), val.h, val.v)) return in_helper(e);  // "write memory"
+        return 0;
+      }
+      return helper_errno_result(L, -14);
+    }
+    case 89: {  // MapPeekElement :335-374: R2 := Lookup(IMM 0 key) — nil when the lookup failed
+      uint32_t m;
+      if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
+      if (!m) return 0;
+      XeReg out;
+      int64_t err;
+      if (int e = map_lookup(L, P, m, XeReg{0, 0, XE_KIND_IMM}, true, out, err)) return in_helper(e);
+      reg_replace(L, 0, XE_KIND_IMM, 0, err, 0);
+      if (err) reg_replace(L, 2, XE_KIND_NIL, 0, 0, 0);
+      else reg_put(L, 2, out);
+      return 0;
+    }
+#else
     case 12: case 25: case 87: case 88: case 89: return XE_EV_UNSUP;
+#endif
   }
   return XE_E_NO_HELPER;
 }
@@ -1092,7 +1704,7 @@ XE_DEV bool jmp_cond(uint32_t op, bool wide, int64_t d, int64_t s) {
 
 // effective offset of a pointer register + insn offset (inst_load.go:91-101)
 XE_DEV int64_t ptr_eff(const XeReg& R, int32_t ioff) {
-  return XE_T_KIND(R.t) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(256, R.v), ioff) : xe_wadd(R.v, ioff);
+  return XE_T_KIND(R.t) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(XE_FRAME, R.v), ioff) : xe_wadd(R.v, ioff);
 }
 
 // ---- per-class handlers (exec_uop dispatches; the JIT calls them directly with constant uops)
@@ -1100,7 +1712,9 @@ XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = 
   const int d = u.dst, s = u.src;
   const bool wide = u.fl & UF_WIDE, reg = u.fl & UF_REG;
   const XeReg D = reg_get(L, d);
+  XE_NILCHK(D);
   const XeReg S = reg ? reg_get(L, s) : XeReg{int64_t(u.imm), 0, 0};
+  if (reg) XE_NILCHK(S);
   if (reg && u.x == 0x00 && XE_T_KIND(S.t) != XE_KIND_IMM) {
     // inst_add.go:82-98,131-147: dst becomes a Copy of the pointer src with the sum as offset
     int64_t v = wide ? xe_wadd(D.v, S.v) : int64_t(int32_t(uint32_t(xe_i32(D.v)) + uint32_t(xe_i32(S.v))));
@@ -1120,18 +1734,22 @@ XE_DEV int uop_movi(XeLane& L, const XeUop& u) {
 
 XE_DEV int uop_movr(XeLane& L, const XeUop& u) {
   const XeReg S = reg_get(L, u.src);
+  XE_NILCHK(S);
   reg_replace(L, u.dst, XE_T_KIND(S.t), S.h, S.v, 0);
   return 0;
 }
 
 XE_DEV int uop_neg(XeLane& L, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
-  const int64_t dv = reg_get(L, u.dst).v;
-  int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(xe_i32(dv))));
+  const XeReg D = reg_get(L, u.dst);
+  XE_NILCHK(D);
+  int64_t v = (u.fl & UF_WIDE) ? int64_t(0ull - uint64_t(D.v)) : int64_t(int32_t(0u - uint32_t(xe_i32(D.v))));
   return reg_inplace(L, u.dst, v, cmd);
 }
 
 XE_DEV int uop_end(XeLane& L, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
-  uint64_t rv = uint64_t(reg_get(L, u.dst).v), v;
+  const XeReg D = reg_get(L, u.dst);
+  XE_NILCHK(D);
+  uint64_t rv = uint64_t(D.v), v;
   if (u.x == 0) {
     v = u.imm == 16 ? uint64_t(__builtin_bswap16(uint16_t(rv)))
       : u.imm == 32 ? uint64_t(__builtin_bswap32(uint32_t(rv))) : __builtin_bswap64(rv);
@@ -1141,7 +1759,7 @@ XE_DEV int uop_end(XeLane& L, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   return reg_inplace(L, u.dst, int64_t(v), cmd);
 }
 
-// returns whether the branch is taken
+// returns whether the branch is taken (nil operands are checked by the caller: jmp_nil)
 XE_DEV bool uop_jmp(const XeLane& L, const XeUop& u) {
   const bool wide = u.fl & UF_WIDE;
   const XeReg D = reg_get(L, u.dst);
@@ -1154,6 +1772,11 @@ XE_DEV bool uop_jmp(const XeLane& L, const XeUop& u) {
   bool imm = XE_T_KIND(D.t) == XE_KIND_IMM;
   bool c = jmp_cond(u.x, wide, D.v, int64_t(u.imm));
   return u.x == 0x50 ? (!imm || c) : (imm && c);
+}
+XE_DEV int jmp_nil(const XeLane& L, const XeUop& u) {
+  XE_NILCHK(reg_get(L, u.dst));
+  if (u.fl & UF_REG) XE_NILCHK(reg_get(L, u.src));
+  return 0;
 }
 
 XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
@@ -1184,6 +1807,7 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm
 
 XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cms = XE_CM_ALL) {
   const XeReg S = reg_get(L, u.src);
+  XE_NILCHK(S);
   if ((cms & XE_CM_IMM) && XE_T_KIND(S.t) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
   uint32_t kind, oh, al; int64_t v;
   if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), true, kind, oh, v, al, cms)) return e;
@@ -1194,28 +1818,33 @@ XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cms = 
 
 // ST (u.cls == U_ST, value = imm) and STX
 XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
-  const XeReg D = reg_get(L, u.dst);
-  if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
   const bool st = u.cls == U_ST;
   const XeReg S = st ? XeReg{int64_t(u.imm), 0, uint32_t(XE_KIND_IMM)} : reg_get(L, u.src);
+  XE_NILCHK(S);  // STX: src.Copy() before the destination (inst_store.go:64-70)
+  const XeReg D = reg_get(L, u.dst);
+  XE_NILCHK(D);
+  if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
   return mem_write(L, P, D.h, ptr_eff(D, u.tgt), uop_size(u), XE_T_KIND(S.t), S.h, S.v, cmd);
 }
 
 XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const XeReg D = reg_get(L, u.dst);
+  XE_NILCHK(D);
   if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
   const uint32_t h = D.h;
   const int64_t off = ptr_eff(D, u.tgt);
   const int size = uop_size(u);
   const uint32_t c = xe_h_cls(h);
-  if ((cmd & XE_CM_VM) && (c == XE_H_CTX || c == XE_H_STACK)) {
+  if ((cmd & XE_CM_VM) && is_vm_cls(c)) {
     int id = 0;
     if (int e = vmem_read(L, h, off, size, id)) return e;
     if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+    const XeReg S = reg_get(L, u.src);
+    XE_NILCHK(S);
     int64_t ov; uint32_t oh, ot;
     obj_get(L, id, ov, oh, ot);
     if (XE_T_KIND(ot) == XE_KIND_FRAMEPTR && (ot & XE_T_RO)) return XE_E_READONLY;
-    int64_t nv = xe_wadd(ov, reg_get(L, u.src).v);
+    int64_t nv = xe_wadd(ov, S.v);
     obj_set_val(L, id, nv);
     alias_refresh(L, uint32_t(id), nv);
     return 0;
@@ -1223,7 +1852,12 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd
   if ((cmd & XE_CM_PKT) && c == XE_H_PKT) {
     if (int e = bounds(off, size, L.plen)) return e;
     if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
-    pkt_store(L, off, size, pkt_load(L, off, size) + uint64_t(reg_get(L, u.src).v));
+    const XeReg S = reg_get(L, u.src);
+    XE_NILCHK(S);
+#if XE_GEN
+    if (int e = bm_before_write(L, P, h)) return e;
+#endif
+    pkt_store(L, off, size, pkt_load(L, off, size) + uint64_t(S.v));
     return 0;
   }
   if (!(cmd & XE_CM_MAPS)) return XE_EV_UNSUP;  // excluded by the class analysis (never reached)
@@ -1231,16 +1865,107 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
   if (u.fl & UF_BADSRC) return XE_E_BAD_REG;
+  const XeReg S = reg_get(L, u.src);
+  XE_NILCHK(S);
+#if XE_GEN
+  if (int e = bm_prepare_write(L, P, h)) return e;
+  if (!B.map) {  // a lane-private ByteMemory: a plain read, add, write
+    bmem_resolve(L, P, h, B);
+    store_le(B.base + off, size, load_le(B.base + off, size) + uint64_t(S.v));
+    return 0;
+  }
+#endif
   fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
   width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
-  wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(reg_get(L, u.src).v));
+  wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(S.v));
   return 0;
 }
 
 XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
                       uint32_t cm3 = XE_CM_ALL) {
-  return call_helper(L, P, u.cls == U_HELPER ? int64_t(u.imm) : reg_get(L, u.dst).v, cm1, cm2, cm3);
+  int64_t fn = int64_t(u.imm);
+  if (u.cls == U_CALLX) {
+    const XeReg F = reg_get(L, u.dst);
+    XE_NILCHK(F);
+    fn = F.v;
+  }
+  return call_helper(L, P, fn, cm1, cm2, cm3);
 }
+
+#if XE_GEN
+// ---- bpf-to-bpf calls (general model)
+// RegisterValue.Clone of a pointer's memory (registers.go:233-240,294-303): a ValueMemory is copied
+// slot by slot (the objects stay shared, memory.go:109-116); a ByteMemory becomes a lane-private
+// ByteMemory that reads through to its source until either is written (memory.go:212-219).
+XE_COLD int clone_mem(XeLane& L, const XeParams& P, uint32_t h, uint32_t& out) {
+  const uint32_t c = xe_h_cls(h);
+  if (is_vm_cls(c)) {
+    const XeVR R = vmem_region(L, h);
+    const int k = vc_alloc(L);
+    if (k < 0) return XE_EV_CAP;
+#pragma unroll 1
+    for (int64_t s = 0; s < R.len; s++)
+      *gat<uint16_t>(L, L.G->o_vc, uint64_t(k) * XE_FRAME + uint64_t(s)) = uint16_t(vmem_id(L, R, s));
+    const uint32_t src = c == XE_H_VCLONE ? vc_src(L, xe_h_slot(h)) : c;
+    *gat<uint32_t>(L, L.G->o_vcinfo, uint32_t(k)) = uint32_t(R.len) | (src << 16);
+    out = xe_h_make(XE_H_VCLONE, 0, uint32_t(k));
+    return 0;
+  }
+  const int k = bm_alloc(L);
+  if (k < 0) return XE_EV_CAP;
+  XeBMem B;
+  bmem_resolve(L, P, h, B);
+  uint32_t info;
+  if (c == XE_H_BMEM) info = *bm_field(L, xe_h_slot(h), XE_BM_INFO);
+  else if (c == XE_H_PKT) info = XE_REGION_PACKET;
+  else if (c == XE_H_ARRAY) info = XE_REGION_ARRAY | (xe_h_map(h) << 8);
+  else if (c == XE_H_HASH) info = XE_REGION_HASHVAL | (xe_h_map(h) << 8);
+  else info = (map_desc(L, xe_h_map(h)).kind == XE_DM_PERF ? XE_REGION_PERF : XE_REGION_QUEUEVAL) | (xe_h_map(h) << 8);
+  *bm_field(L, uint32_t(k), XE_BM_SRC) = bm_ident(h);
+  *bm_field(L, uint32_t(k), XE_BM_MAT) = XE_NONE;
+  *bm_field(L, uint32_t(k), XE_BM_LEN) = uint32_t(B.len);
+  *bm_field(L, uint32_t(k), XE_BM_INFO) = info;
+  L.npristine++;
+  out = xe_h_make(XE_H_BMEM, 0, uint32_t(k));
+  return 0;
+}
+
+// CallBPF, emulator/inst_call_bpf.go:18-44: push Registers.Clone() (only its PC and R6..R9 are ever
+// restored), move R10 to the next, wiped, stack frame, jump. The clone happens first, so a nil register
+// panics even when the frame index then overflows.
+XE_COLD int uop_callbpf(XeLane& L, const XeParams& P, const XeUop& u, int32_t pc, int32_t& tgt) {
+#pragma unroll 1
+  for (int r = 0; r < 10; r++) XE_NILCHK(reg_get(L, r));
+  if (L.npres + 1 >= XE_MAX_FRAMES || L.npres + 1 >= L.G->nframes) return XE_EV_PANIC | XE_P_INDEX;  // &StackFrames[Index+1]
+  const uint32_t e = L.npres;
+#pragma unroll 1
+  for (int r = 6; r < 10; r++) {
+    const XeReg R = reg_get(L, r);
+    XeReg C{R.v, 0, XE_T_KIND(R.t) | (XE_T_KIND(R.t) == XE_KIND_FRAMEPTR ? (R.t & XE_T_RO) : 0u)};
+    if (XE_ISPTR(R.t))
+      if (int err = clone_mem(L, P, R.h, C.h)) return err;
+    pres_put(L, e, r - 6, C);
+  }
+  *pres_word(L, e, 0) = uint32_t(pc);
+  L.npres = e + 1;
+  const int bit = int(L.npres) * 16;  // wipe frame npres: all its groups read as nil again
+  L.fdirty[bit >> 6] &= ~(0xffffull << (bit & 63));
+  reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, L.npres, 0), 0, XE_T_RO);
+  tgt = pc + u.imm;
+  return 0;
+}
+
+// Exit, emulator/inst_exit.go:22-48: inside a call, restore PC, R6..R9 (the clones) and R10.
+XE_DEV int uop_exit(XeLane& L, int32_t& tgt) {
+  if (L.npres == 0) return XE_EV_EXIT;
+  const uint32_t e = --L.npres;
+#pragma unroll 1
+  for (int r = 6; r < 10; r++) reg_put(L, r, pres_get(L, e, r - 6));
+  reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, L.npres, 0), 0, XE_T_RO);
+  tgt = int32_t(*pres_word(L, e, 0));
+  return 0;
+}
+#endif
 
 // ------------------------------------------------------------------ one instruction
 // Executes uop u (at pc) on this lane. Returns 0 (continue; `tgt` = PC after the instruction,
@@ -1250,22 +1975,39 @@ XE_DEV int exec_uop(XeLane& L, const XeParams& P, const XeUop& u, int32_t pc, in
   switch (u.cls) {
     case U_FAIL: return u.imm;
     case U_NOP: return 0;
+#if XE_GEN
+    case U_EXIT: return uop_exit(L, tgt);
+#else
     case U_EXIT: return XE_EV_EXIT;
+#endif
     case U_JA: tgt = u.tgt; return 0;
     case U_ALU: return uop_alu(L, P, u);
     case U_MOVI: return uop_movi(L, u);
     case U_MOVR: return uop_movr(L, u);
     case U_NEG: return uop_neg(L, u);
     case U_END: return uop_end(L, u);
-    case U_JMP: if (uop_jmp(L, u)) tgt = u.tgt; return 0;
+    case U_JMP:
+      if (int e = jmp_nil(L, u)) return e;
+      if (uop_jmp(L, u)) tgt = u.tgt;
+      return 0;
     case U_LDIMM64: return uop_ldimm64(L, P, u);
     case U_LDX: return uop_ldx(L, P, u);
     case U_ST:
     case U_STX: return uop_store(L, P, u);
     case U_ATOMIC: return uop_atomic(L, P, u);
     case U_HELPER:
-    case U_CALLX: return uop_helper(L, P, u);
+    case U_CALLX: {
+      int e = uop_helper(L, P, u);
+#if XE_HAS_ORDERED
+      if (e == XE_EV_JUMP) { tgt = -1; return 0; }  // tail call: PC := -1 in the new program
+#endif
+      return e;
+    }
+#if XE_GEN
+    case U_CALLBPF: return uop_callbpf(L, P, u, pc, tgt);
+#else
     case U_CALLBPF: return XE_EV_UNSUP;
+#endif
   }
   return XE_EV_UNSUP;
 }
@@ -1357,8 +2099,19 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   for (int r = 0; r < 10; r++) reg_replace(L, r, XE_KIND_IMM, 0, 0, 0);
   reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
   reg_replace(L, 1, XE_KIND_MEMPTR, xe_h_make(XE_H_CTX, 0, 0), 0, 0);
+#if !XE_GEN
   L.dirty = 0;
   L.oused = 0x7full | (XE_OBJ_LIMIT >= 64 ? 0ull : (~0ull << (XE_OBJ_LIMIT & 63)));
+#else
+  L.onext = 7;  // ids 1..6: the xdp_md objects
+  L.ofree = L.vnext = L.vfree = L.bnext = L.bfree = 0;
+  L.bused = 0;
+  L.fdirty[0] = L.fdirty[1] = 0;
+  L.ctxdirty = 0;
+  L.npres = 0;  // the harness sets PreservedRegisters = nil
+  L.pi = P.entry;
+  L.npristine = 0;
+#endif
   L.odef = 0x7eull;
   L.pkt = P.umem;
   L.plen = 0;
@@ -1442,7 +2195,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
 XE_DEV void status_from_error(int e, int& status, int& code) {
   if (e == XE_EV_EXIT) { status = XE_ST_OK; }
   else if (XE_EV_CLASS(e) == XE_EV_ORD) { status = XE_ST_INTERNAL_ORDERED; }
-  else if (XE_EV_CLASS(e) == XE_EV_CAP) { status = XE_ST_CAPACITY; }
+  else if (XE_EV_CLASS(e) == XE_EV_CAP) { status = XE_ST_INTERNAL_CAPACITY; }
   else if (XE_EV_CLASS(e) == XE_EV_UNSUP) { status = XE_ST_UNSUPPORTED; }
   else if (XE_IS_PANIC(e)) { status = XE_ST_PANIC; code = e & 0xff; }
   else { status = XE_ST_VMERR; code = e & 0xffff; }
@@ -1452,7 +2205,7 @@ XE_DEV void status_from_error(int e, int& status, int& code) {
 XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, int status, int code,
                         int32_t res_pc, uint64_t steps) {
   if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
-  if (status == XE_ST_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
+  if (status == XE_ST_INTERNAL_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
   if (valid) {
     const XeReg R0 = reg_get(L, 0);
     if (P.results) {
@@ -1473,11 +2226,17 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
         g.val[r] = R.v;
         uint32_t k = XE_T_KIND(R.t);
         g.kind[r] = uint8_t(k);
-        if (k == XE_KIND_IMM) { g.region[r] = 0xff; g.map[r] = 0; }
+        if (k == XE_KIND_IMM || k == XE_KIND_NIL) { g.region[r] = 0xff; g.map[r] = 0; }
         else {
-          uint32_t c = xe_h_cls(R.h);
-          g.region[r] = uint8_t(c);
-          g.map[r] = uint8_t((c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(R.h) : 0);
+          uint32_t c = xe_h_cls(R.h), rg = c, mp = (c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(R.h) : 0;
+#if XE_GEN
+          // clones report the region of the memory they copied (Clone keeps it, memory.go:109-116,212-219)
+          if (c == XE_H_VCLONE) { rg = vc_src(L, xe_h_slot(R.h)); mp = 0; }
+          else if (c == XE_H_BMEM) { const uint32_t inf = *bm_field(L, xe_h_slot(R.h), XE_BM_INFO); rg = inf & 0xff; mp = inf >> 8; }
+          else if (c == XE_H_QVAL) { rg = map_desc(L, xe_h_map(R.h)).kind == XE_DM_PERF ? XE_REGION_PERF : XE_REGION_QUEUEVAL; mp = xe_h_map(R.h); }
+#endif
+          g.region[r] = uint8_t(rg);
+          g.map[r] = uint8_t(mp);
         }
       }
       g.pad[0] = g.pad[1] = 0;
@@ -1508,6 +2267,10 @@ XE_DEV void stage_maps(XeLane& L, const XeParams& P, XE_LP(XeDevMap) lds) {
 }
 
 XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
+#if XE_GEN
+  L.G = &P.gen;
+  L.gl = P.mode == XE_MODE_SEQUENTIAL ? 0u : wave * XE_WAVE + uint32_t(xe_lane());
+#endif
   L.rep = P.rep + uint64_t(wave % P.nrep) * P.rep_words;
   L.wave = wave;
   L.awidth = 0;
@@ -1521,8 +2284,15 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   for (int st = 0; st < 8; st++) L.acc_status[st] = 0;
 }
 
-// Interpreter engine: runs the harness for the staged packet `i` on this lane (valid=false: the lane
-// idles). All lanes of the wave must call this together.
+#if XE_GEN
+#define XE_LANE_PI(L) ((L).pi)
+#else
+#define XE_LANE_PI(L) (P.entry)
+#endif
+// Interpreter engine (general model): runs the harness for the staged packet `i` on this lane
+// (valid=false: the lane idles). All lanes of the wave must call this together. A lane's position is
+// (program index, PC): the wave runs the lanes at the smallest index into the concatenated program
+// table, so lanes that tail-called into another program keep their own stream.
 XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   int status = valid ? -1 : XE_ST_OK;  // -1 = running
   int code = 0;
@@ -1530,29 +2300,35 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   uint64_t steps = 0;
 
   for (;;) {
-    int mypc = status == -1 ? pc : 0x7fffffff;
-    int sel = wave_min(mypc);
-    if (sel == 0x7fffffff) break;
-    if (status == -1 && pc == sel) {
+    int key = 0x7fffffff;
+    if (status == -1) {
       if (steps >= P.max_steps) {
-        status = XE_ST_BUDGET; res_pc = pc;
-      } else if (sel < 0 || sel >= P.prog_len) {
+        status = XE_ST_BUDGET; res_pc = pc;  // the Go VM has no budget: it would run on
+      } else if (XE_LANE_PI(L) < 1 || XE_LANE_PI(L) > int32_t(P.nprogs)) {
+        status = XE_ST_VMERR; code = XE_E_NO_PROGRAM; res_pc = pc;  // vm.go:138-140
+      } else if (pc < 0 || pc >= P.prog_lens[XE_LANE_PI(L)]) {
         status = XE_ST_PANIC; code = XE_P_INDEX; res_pc = pc;  // program[PC] (vm.go:143)
       } else {
-        const XeUop u = P.prog[sel];  // wave-uniform: scalar load
-        steps++;
-        int32_t tgt;
-        int e = exec_uop(L, P, u, sel, tgt);
-        res_pc = sel;
-        if (e == 0) {
-          if (int64_t(P.prog_len) <= int64_t(tgt) + 1) {  // vm.go:162-167
-            status = XE_ST_VMERR; code = XE_E_BAD_PC;
-          } else {
-            pc = tgt + 1;
-          }
+        key = P.prog_off[XE_LANE_PI(L)] + pc;
+      }
+    }
+    const int sel = wave_min(key);
+    if (sel == 0x7fffffff) break;
+    if (key == sel) {
+      const XeUop u = P.progs[sel];  // wave-uniform: scalar load
+      const int32_t plen = P.prog_lens[XE_LANE_PI(L)];  // Step's `program` (vm.go:141)
+      steps++;
+      int32_t tgt;
+      int e = exec_uop(L, P, u, pc, tgt);
+      res_pc = pc;
+      if (e == 0) {
+        if (int64_t(plen) <= int64_t(tgt) + 1) {  // vm.go:162-167
+          status = XE_ST_VMERR; code = XE_E_BAD_PC;
         } else {
-          status_from_error(e, status, code);
+          pc = tgt + 1;
         }
+      } else {
+        status_from_error(e, status, code);
       }
     }
   }

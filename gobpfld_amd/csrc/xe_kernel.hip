@@ -1,8 +1,9 @@
 // xe_kernel.hip — gfx950 kernels of the batched eBPF/XDP emulator.
 //
-// xe_interp_kernel: one lane per packet (wave64), grid-stride over 64-packet chunks in parallel
-// mode (software-pipelined, parallel_packets); a single lane walking the packets in order in sequential mode (exact fallback for
-// order-dependent map effects). xe_delta_kernel / xe_apply_delta_kernel: u64 counter deltas for
+// xe_interp_kernel: the shared micro-op interpreter over the general lane model (every program: loops,
+// bpf-to-bpf calls, tail calls, the ordered maps). One lane per packet (wave64), grid-stride over
+// 64-packet chunks in parallel mode (software-pipelined, parallel_packets); a single lane walking the
+// packets in order in sequential mode (exact fallback for order-dependent map effects). xe_delta_kernel / xe_apply_delta_kernel: u64 counter deltas for
 // the multi-GPU all-reduce.
 #include "xe_interp.h"
 
@@ -10,9 +11,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[4 * XE_HDR_WAVE_BYTES];
   __shared__ XePend pend_lds[4];
   extern __shared__ __attribute__((aligned(16))) uint8_t xe_dyn_lds[];  // (nmaps + 1) map descriptors
-  XeMem M;
-  XeLane L;
-  L.mem = &M;
+  XeLane L;  // general lane model: objects, frames and clones in the P.gen arena
   L.hdrbuf = (XE_LP(uint8_t))(hdr_lds + (threadIdx.x >> 6) * XE_HDR_WAVE_BYTES);
   const int lane = xe_lane();
   stage_maps(L, P, (XE_LP(XeDevMap))xe_dyn_lds);

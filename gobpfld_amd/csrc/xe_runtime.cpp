@@ -34,11 +34,13 @@ extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, ui
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
-                            const char** err);
+                            bool* general, const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
 #endif
+
+#define XE_FRAME_SIZE 256  // DefaultVMSettings().StackFrameSize (emulator/vm.go:291-296)
 
 namespace {
 
@@ -52,9 +54,7 @@ int d2d(void* d, const void* s, size_t n, xe_stream_t) { memmove(d, s, n); retur
 int dmemset(void* d, int v, size_t n, xe_stream_t) { memset(d, v, n); return 0; }
 int dsync(xe_stream_t) { return 0; }
 int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
-  XeMem M;
   XeLane L;
-  L.mem = &M;
   static thread_local uint8_t hdrbuf[XE_HDR_WAVE_BYTES];  // one per host thread (xe_multi runs shards concurrently)
   L.hdrbuf = hdrbuf;
   XePend pend;
@@ -339,6 +339,24 @@ struct HostMap {
   uint32_t wclass = 0;  // width classes of the last run's adds (bit 0: 1 B ... bit 3: 8 B)
   uint32_t live = 0;    // HASH: entry count for replica sizing (host count, refreshed after ordered runs)
   bool host_dirty = true, dev_dirty = false;
+  // ordered maps (LRU_HASH / QUEUE / STACK / PERF_EVENT_ARRAY): the host mirror in Go order —
+  // LRU: the UsageList (most recently used first) with each key's value; QUEUE / STACK: the Values
+  // slice; PERF: the Events slice. An empty `val` is a nil backing (length 0).
+  struct Rec {
+    std::vector<uint8_t> key;
+    bool nil_key = false;
+    std::vector<uint8_t> val;
+  };
+  std::vector<Rec> items;
+  bool stack = false;
+  uint64_t* d_hdr = nullptr;
+  uint32_t* d_link = nullptr;
+  uint32_t* d_elen = nullptr;
+  uint64_t* d_rec = nullptr;
+  uint32_t pool_cap = 0, list_cap = 0;  // capacities of the device copy (grown on XE_FLAG_CAPACITY)
+  uint64_t data_cap = 0;
+  uint64_t n_vals = 0, n_elen = 0, n_link = 0, n_rec = 0;  // allocated elements of the device arrays
+  bool ordered() const { return dkind == XE_DM_LRU || dkind == XE_DM_LIST || dkind == XE_DM_PERF; }
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
   void pack_key(const void* key, uint64_t* kw) const {
@@ -397,9 +415,21 @@ struct xe_vm {
   std::string last_error;
   xe_stream_t stream = nullptr;
   // device buffers
-  XeUop* d_prog = nullptr;
-  int32_t d_prog_idx = -1;
-  size_t d_prog_len = 0;
+  // every program, concatenated (tail calls switch programs): uops + per-program offset / length
+  XeUop* d_progs = nullptr;
+  int32_t* d_prog_off = nullptr;  // [0..P]: offsets, then [P+1..2P+1]: lengths
+  size_t d_progs_n = 0;           // programs uploaded
+  size_t d_prog_len = 0;          // length of the entry program
+  std::vector<int32_t> prog_off;
+  // general lane model arenas (XeGen): parallel launches (one slot per thread of the grid) and the
+  // ordered replay (one lane, large capacities, x4 per XE_FLAG_CAPACITY)
+  uint8_t* d_arena_par = nullptr;
+  uint64_t arena_par_bytes = 0;
+  uint8_t* d_arena_seq = nullptr;
+  uint64_t arena_seq_bytes = 0;
+  uint32_t seq_scale = 1;
+  uint64_t* d_ksnap = nullptr;  // HASH slot records + counts before an ordered replay (its rollback point)
+  size_t d_ksnap_bytes = 0;
   XeDevMap* d_maps = nullptr;
   size_t d_maps_n = 0;
   std::vector<XeDevMap> dm_uploaded;  // host copy of the device map table (upload only on change)
@@ -424,8 +454,12 @@ struct xe_vm {
   size_t jit_nmaps = 0;
   void* jit_fn = nullptr;
   bool jit_cyclic = false;
+  bool jit_general = false;  // the per-program kernel uses the general lane model (loops, > 57 objects)
   std::string jit_error;
   Timer t0, t1, t2;
+  // room the ordered maps' device copies keep for one run (elements / events, event bytes), grown
+  // ×4 when a run reports XE_FLAG_CAPACITY
+  uint64_t ord_slack = 4096, ord_slack_bytes = 1 << 20;
 };
 
 namespace {
@@ -457,17 +491,19 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 // 1M-entry table) needs >= 4 (1 replica: 8.2 ms, 2: 1.1-4.0 ms depending on placement, 4: 1.08 ms);
 // C5 (1M uniform flows) is fastest with none (3.45 ms; each doubling costs ~5 %).
 uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc) {
-  if (const char* e = getenv("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));  // tuning experiments
+  if (const char* e = xe_tuning_env("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));
   uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
   while (want > 1 && uint64_t(want) * vals_alloc > (128ull << 20)) want >>= 1;
   return want;
 }
 
 int map_alloc_device(HostMap& m) {
+  if (m.ordered()) return 0;  // sized at upload (ordered_upload)
   if (dev_alloc((void**)&m.d_vals, m.vals_alloc)) return -1;
   if (dev_alloc((void**)&m.d_snap, m.vals_alloc)) return -1;
   m.nrep = 1;  // replicas are sized per run (set_replicas)
   m.rep_stride = (m.vals_alloc + 255) & ~uint64_t(255);
+  if (const char* e = xe_tuning_env("XE_REP_SKEW")) m.rep_stride = ((m.vals_alloc + 4095) & ~uint64_t(4095)) + uint64_t(atoll(e));
   if (m.dkind == XE_DM_HASH) {
     if (dev_alloc((void**)&m.d_keys, size_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8)) return -1;
     if (dev_alloc((void**)&m.d_count, 8)) return -1;
@@ -478,9 +514,20 @@ int map_alloc_device(HostMap& m) {
 void map_free_device(HostMap& m) {
   dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count); dev_free(m.d_rep);
   m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr; m.d_rep = nullptr;
+  dev_free(m.d_hdr); dev_free(m.d_link); dev_free(m.d_elen); dev_free(m.d_rec);
+  m.d_hdr = nullptr; m.d_link = nullptr; m.d_elen = nullptr; m.d_rec = nullptr;
+  m.pool_cap = m.list_cap = 0;
+  m.data_cap = 0;
+  m.n_vals = m.n_elen = m.n_link = m.n_rec = 0;
 }
 
+// Ordered maps on the device (xe_interp.h, general model; XeDevMap comment): rebuilt from the host
+// mirror with room for `slack` more elements / events (and slack_bytes more event bytes).
+int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes);
+int ordered_download(xe_vm* vm, HostMap& m);
+
 int map_upload(xe_vm* vm, HostMap& m) {
+  if (m.ordered()) return ordered_upload(vm, m, vm->ord_slack, vm->ord_slack_bytes);
   if (h2d(m.d_vals, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
   // the delta base is the uploaded state until a run takes its own snapshot
   if (h2d(m.d_snap, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
@@ -504,6 +551,11 @@ int map_upload(xe_vm* vm, HostMap& m) {
 
 int map_download(xe_vm* vm, HostMap& m) {
   if (!m.dev_dirty) return 0;
+  if (m.ordered()) {
+    if (ordered_download(vm, m)) return -1;
+    m.dev_dirty = false;
+    return 0;
+  }
   if (d2h(m.vals.data(), m.d_vals, m.vals_alloc, vm->stream)) return -1;
   if (m.dkind == XE_DM_HASH) {
     const uint32_t rw = xe_hash_rwords(m.kwords);
@@ -521,6 +573,157 @@ int map_download(xe_vm* vm, HostMap& m) {
   return 0;
 }
 
+// host-side slot of `key` in an open-addressing table of `cap` slots laid out like the device's
+// (xe_hash_words, linear probing; the nil key takes slot cap)
+uint32_t host_probe(const std::vector<uint64_t>& rec, uint32_t rw, uint32_t cap, const uint64_t* kw, uint32_t kwords,
+                    uint32_t key_size) {
+  uint32_t idx = uint32_t(xe_hash_words(kw, kwords, key_size)) & (cap - 1);
+  while (rec[size_t(idx) * rw] & XE_SLOT_FULL) idx = (idx + 1) & (cap - 1);
+  return idx;
+}
+
+template <class T>
+int ensure_dev(T** p, uint64_t& have, uint64_t need_elems) {  // grow-only device array
+  if (*p && have >= need_elems) return 0;
+  dev_free(*p);
+  *p = nullptr;
+  if (dev_alloc((void**)p, size_t(std::max<uint64_t>(need_elems, 1)) * sizeof(T))) { have = 0; return -1; }
+  have = need_elems;
+  return 0;
+}
+
+int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) {
+  const uint64_t n = m.items.size();
+  const uint32_t vs = m.def.value_size;
+  xe_stream_t st = vm->stream;
+  std::vector<uint64_t> hdr(8, 0);
+  if (m.dkind == XE_DM_PERF) {
+    std::vector<uint64_t> rec(2 * (n + slack), 0);
+    uint64_t used = 0;
+    for (uint64_t i = 0; i < n; i++) { rec[2 * i] = used; rec[2 * i + 1] = m.items[i].val.size(); used += (m.items[i].val.size() + 7) & ~7ull; }
+    std::vector<uint8_t> data(std::max<uint64_t>(used, 8), 0);
+    for (uint64_t i = 0; i < n; i++) if (!m.items[i].val.empty()) memcpy(&data[rec[2 * i]], m.items[i].val.data(), m.items[i].val.size());
+    if (ensure_dev(&m.d_rec, m.n_rec, 2 * (n + slack))) return -1;
+    if (ensure_dev(&m.d_vals, m.n_vals, used + slack_bytes + 8)) return -1;
+    m.pool_cap = uint32_t(n + slack);
+    m.data_cap = used + slack_bytes;
+    hdr[0] = n; hdr[1] = used;
+    if (h2d(m.d_rec, rec.data(), rec.size() * 8, st) || h2d(m.d_vals, data.data(), data.size(), st)) return -1;
+  } else {
+    const uint64_t pool = n + slack;
+    std::vector<uint8_t> vals(std::max<uint64_t>(pool * vs, 8), 0);
+    std::vector<uint32_t> elen(pool, 0);
+    for (uint64_t i = 0; i < n; i++) {
+      elen[i] = uint32_t(m.items[i].val.size());
+      if (elen[i]) memcpy(&vals[i * vs], m.items[i].val.data(), std::min<size_t>(vs, m.items[i].val.size()));
+    }
+    std::vector<uint32_t> link;
+    if (m.dkind == XE_DM_LRU) {
+      const uint32_t rw = xe_hash_rwords(m.kwords);
+      std::vector<uint64_t> rec(size_t(m.cap + 1) * rw, 0);
+      link.assign(4 * pool, XE_NONE);
+      for (uint64_t i = 0; i < n; i++) {
+        uint32_t slot = m.cap;
+        if (!m.items[i].nil_key) {
+          uint64_t kw[XE_MAX_KEY / 8] = {0};
+          memcpy(kw, m.items[i].key.data(), m.def.key_size);
+          slot = host_probe(rec, rw, m.cap, kw, m.kwords, m.def.key_size);
+          for (uint32_t w = 0; w < m.kwords; w++) rec[size_t(slot) * rw + 1 + w] = kw[w];
+        }
+        rec[size_t(slot) * rw] = XE_SLOT_FULL | (i << 32);
+        link[4 * i] = i ? uint32_t(i - 1) : XE_NONE;
+        link[4 * i + 1] = i + 1 < n ? uint32_t(i + 1) : XE_NONE;
+        link[4 * i + 2] = slot;
+      }
+      if (!m.d_keys && dev_alloc((void**)&m.d_keys, rec.size() * 8)) return -1;
+      if (h2d(m.d_keys, rec.data(), rec.size() * 8, st)) return -1;
+      hdr[0] = n ? 0 : XE_NONE; hdr[1] = n ? n - 1 : XE_NONE; hdr[2] = n; hdr[3] = n;
+    } else {  // QUEUE / STACK: element i is Values[i]; the list starts at 0
+      link.resize(pool);
+      for (uint64_t i = 0; i < pool; i++) link[i] = uint32_t(i);
+      hdr[0] = 0; hdr[1] = n; hdr[2] = n; hdr[4] = m.stack ? 1 : 0;
+      m.list_cap = uint32_t(pool);
+    }
+    if (ensure_dev(&m.d_vals, m.n_vals, pool * vs + 8) || ensure_dev(&m.d_elen, m.n_elen, pool) ||
+        ensure_dev(&m.d_link, m.n_link, link.size()))
+      return -1;
+    m.pool_cap = uint32_t(pool);
+    if (h2d(m.d_vals, vals.data(), vals.size(), st) || h2d(m.d_elen, elen.data(), elen.size() * 4, st) ||
+        h2d(m.d_link, link.data(), link.size() * 4, st))
+      return -1;
+  }
+  if (!m.d_hdr && dev_alloc((void**)&m.d_hdr, 8 * 8)) return -1;
+  if (h2d(m.d_hdr, hdr.data(), 64, st) || dsync(st)) return -1;
+  m.host_dirty = false;
+  return 0;
+}
+
+int ordered_download(xe_vm* vm, HostMap& m) {
+  xe_stream_t st = vm->stream;
+  std::vector<uint64_t> hdr(8, 0);
+  if (d2h(hdr.data(), m.d_hdr, 64, st) || dsync(st)) return -1;
+  const uint32_t vs = m.def.value_size;
+  m.items.clear();
+  if (m.dkind == XE_DM_PERF) {
+    const uint64_t n = hdr[0], used = hdr[1];
+    std::vector<uint64_t> rec(2 * n + 2);
+    std::vector<uint8_t> data(used + 8);
+    if (d2h(rec.data(), m.d_rec, 2 * n * 8, st) || d2h(data.data(), m.d_vals, used, st) || dsync(st)) return -1;
+    for (uint64_t i = 0; i < n; i++) {
+      HostMap::Rec r;
+      r.val.assign(data.begin() + long(rec[2 * i]), data.begin() + long(rec[2 * i] + rec[2 * i + 1]));
+      m.items.push_back(std::move(r));
+    }
+    return 0;
+  }
+  const uint64_t pool = m.dkind == XE_DM_LRU ? hdr[3] : hdr[2];
+  std::vector<uint8_t> vals(pool * vs + 8);
+  std::vector<uint32_t> elen(pool + 1);
+  if (d2h(vals.data(), m.d_vals, pool * vs, st) || d2h(elen.data(), m.d_elen, pool * 4, st)) return -1;
+  if (m.dkind == XE_DM_LRU) {
+    const uint32_t rw = xe_hash_rwords(m.kwords);
+    std::vector<uint64_t> rec(size_t(m.cap + 1) * rw);
+    std::vector<uint32_t> link(4 * pool + 4);
+    if (d2h(rec.data(), m.d_keys, rec.size() * 8, st) || d2h(link.data(), m.d_link, 4 * pool * 4, st) || dsync(st)) return -1;
+    for (uint32_t v = uint32_t(hdr[0]); v != XE_NONE; v = link[4 * size_t(v) + 1]) {
+      HostMap::Rec r;
+      const uint32_t slot = link[4 * size_t(v) + 2];
+      r.nil_key = slot == m.cap;
+      if (!r.nil_key) {
+        r.key.resize(m.def.key_size);
+        memcpy(r.key.data(), &rec[size_t(slot) * rw + 1], m.def.key_size);
+      }
+      r.val.assign(vals.begin() + long(size_t(v) * vs), vals.begin() + long(size_t(v) * vs + elen[v]));
+      m.items.push_back(std::move(r));
+    }
+    return 0;
+  }
+  std::vector<uint32_t> link(m.list_cap + 1);
+  if (d2h(link.data(), m.d_link, size_t(m.list_cap) * 4, st) || dsync(st)) return -1;
+  const uint64_t head = hdr[0], cnt = hdr[1];
+  for (uint64_t i = 0; i < cnt; i++) {
+    const uint32_t id = link[m.stack ? i : (head + i) % m.list_cap];
+    HostMap::Rec r;
+    r.val.assign(vals.begin() + long(size_t(id) * vs), vals.begin() + long(size_t(id) * vs + elen[id]));
+    m.items.push_back(std::move(r));
+  }
+  return 0;
+}
+
+// Go semantics of the ordered maps on the host mirror (userspace Map calls): LRU promote / delete
+// (maps_hash_lru.go:51-68,163-183)
+size_t lru_index(const HostMap& m, const std::vector<uint8_t>& key) {
+  for (size_t i = 0; i < m.items.size(); i++)
+    if (!m.items[i].nil_key && m.items[i].key == key) return i;
+  return m.items.size();
+}
+void lru_promote_host(HostMap& m, size_t i) {
+  if (i == 0 || i >= m.items.size()) return;
+  HostMap::Rec r = std::move(m.items[i]);
+  m.items.erase(m.items.begin() + long(i));
+  m.items.insert(m.items.begin(), std::move(r));
+}
+
 HostMap* get_map(xe_vm* vm, int32_t idx) {
   if (!vm || idx < 1 || idx >= int32_t(vm->maps.size())) return nullptr;
   return &vm->maps[idx];
@@ -530,17 +733,29 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   if (vm->entry < 1 || vm->entry >= int32_t(vm->programs.size()))
     return fail(vm, XE_ERR_INVAL, "no program loaded at PI");
   if (set_device(vm->settings.device)) return fail(vm, XE_ERR_DEVICE, "hipSetDevice failed");
-  const auto& prog = vm->programs[vm->entry];
-  if (vm->d_prog_idx != vm->entry) {
-    dev_free(vm->d_prog);
-    vm->d_prog = nullptr;
-    if (dev_alloc((void**)&vm->d_prog, std::max<size_t>(prog.size(), 1) * sizeof(XeUop)))
-      return fail(vm, XE_ERR_DEVICE, "device alloc (program)");
-    if (!prog.empty() && (h2d(vm->d_prog, prog.data(), prog.size() * sizeof(XeUop), vm->stream) || dsync(vm->stream)))
+  if (vm->d_progs_n != vm->programs.size() - 1) {  // program table: every program of the VM
+    const size_t np = vm->programs.size() - 1;
+    std::vector<XeUop> all;
+    std::vector<int32_t> tab(2 * (np + 1), 0);
+    for (size_t p = 1; p <= np; p++) {
+      tab[p] = int32_t(all.size());
+      tab[np + 1 + p] = int32_t(vm->programs[p].size());
+      all.insert(all.end(), vm->programs[p].begin(), vm->programs[p].end());
+    }
+    dev_free(vm->d_progs);
+    dev_free(vm->d_prog_off);
+    vm->d_progs = nullptr;
+    vm->d_prog_off = nullptr;
+    if (dev_alloc((void**)&vm->d_progs, std::max<size_t>(all.size(), 1) * sizeof(XeUop)) ||
+        dev_alloc((void**)&vm->d_prog_off, tab.size() * 4))
+      return fail(vm, XE_ERR_DEVICE, "device alloc (programs)");
+    if ((!all.empty() && h2d(vm->d_progs, all.data(), all.size() * sizeof(XeUop), vm->stream)) ||
+        h2d(vm->d_prog_off, tab.data(), tab.size() * 4, vm->stream) || dsync(vm->stream))
       return fail(vm, XE_ERR_DEVICE, "program upload");
-    vm->d_prog_idx = vm->entry;
-    vm->d_prog_len = prog.size();
+    vm->prog_off = tab;
+    vm->d_progs_n = np;
   }
+  vm->d_prog_len = vm->programs[vm->entry].size();
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.host_dirty && map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
@@ -563,6 +778,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     HostMap& m = vm->maps[i];
     XeDevMap& d = dm[i];
     d.kind = m.dkind;
+    d.btype = m.def.type;
     d.key_size = m.def.key_size;
     d.value_size = m.def.value_size;
     d.max_entries = m.def.max_entries;
@@ -573,10 +789,17 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     d.count = m.d_count;
     d.cap = m.cap;
     d.kwords = m.kwords;
-    d.rwords = m.dkind == XE_DM_HASH ? xe_hash_rwords(m.kwords) : 0;
+    d.rwords = (m.dkind == XE_DM_HASH || m.dkind == XE_DM_LRU) ? xe_hash_rwords(m.kwords) : 0;
     d.rep = m.d_rep;
     d.rep_stride = m.rep_stride;
     d.nrep = m.nrep;
+    d.hdr = m.d_hdr;
+    d.link = m.d_link;
+    d.elen = m.d_elen;
+    d.rec = m.d_rec;
+    d.pool_cap = m.pool_cap;
+    d.list_cap = m.list_cap;
+    d.data_cap = m.data_cap;
   }
   if (vm->d_maps_n < dm.size()) {
     dev_free(vm->d_maps);
@@ -593,6 +816,35 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   return XE_OK;
 }
 
+// ---- general lane model arena (XeGen, xe_internal.h): interleaved per-lane fields, 256-B aligned
+XeGen gen_layout(uint32_t nl, uint32_t nobj, uint32_t nframes, uint32_t nvc, uint32_t nbm, uint64_t nbytes, uint64_t* total) {
+  XeGen g{};
+  g.nl = nl; g.nobj = nobj; g.nframes = nframes; g.nvc = nvc; g.nbm = nbm; g.nbytes = nbytes;
+  g.mark_words = (((nobj + 31) & ~31u) + ((nvc + 31) & ~31u) + ((nbm + 31) & ~31u)) / 32;
+  uint64_t at = 0;
+  auto field = [&](uint64_t& off, uint64_t bytes_per_lane) {
+    off = at;
+    at = (at + bytes_per_lane * nl + 255) & ~uint64_t(255);
+  };
+  field(g.o_ov, 8ull * nobj);
+  field(g.o_oh, 4ull * nobj);
+  field(g.o_ot, 4ull * nobj);
+  field(g.o_ofree, 4ull * nobj);
+  field(g.o_mark, 4ull * g.mark_words);
+  field(g.o_frm, 2ull * XE_FRAME_SIZE * nframes);
+  field(g.o_ctx, 2ull * 24);
+  field(g.o_vc, 2ull * XE_FRAME_SIZE * nvc);
+  field(g.o_vcinfo, 4ull * nvc);
+  field(g.o_vfree, 4ull * nvc);
+  field(g.o_bm, 16ull * nbm);
+  field(g.o_bfree, 4ull * nbm);
+  field(g.o_pres, 4ull * 17 * 8);
+  g.o_key = at;
+  field(g.o_bytes, nbytes);
+  *total = at;
+  return g;
+}
+
 // Parallel-mode grid: exactly the blocks that are resident at once (persistent waves walking the
 // chunks, see parallel_packets), never more than one 64-packet chunk per wave. A second generation of
 // blocks would run its full share after the first finishes, and every extra wave adds its per-wave
@@ -601,7 +853,7 @@ uint32_t grid_blocks(uint32_t n, int per_cu, int cus) {
   uint64_t chunks = (uint64_t(n) + 63) / 64;
   uint64_t blocks = (chunks + 3) / 4;  // 4 waves per 256-thread block
   uint64_t maxb = (per_cu > 0 && cus > 0) ? uint64_t(per_cu) * uint64_t(cus) : 256ull * 4;
-  if (const char* e = getenv("XE_MAX_BLOCKS")) maxb = std::max(1ll, atoll(e));  // tuning experiments
+  if (const char* e = xe_tuning_env("XE_MAX_BLOCKS")) maxb = std::max(1ll, atoll(e));
   return uint32_t(std::max<uint64_t>(1, std::min(blocks, maxb)));
 }
 
@@ -646,7 +898,8 @@ void xe_destroy(xe_vm* vm) {
   if (!vm) return;
   set_device(vm->settings.device);
   for (auto& m : vm->maps) map_free_device(m);
-  dev_free(vm->d_prog); dev_free(vm->d_maps); dev_free(vm->d_aux);
+  dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
+  dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
   dev_free(vm->d_usnap);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
@@ -696,8 +949,22 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
       m.keys.assign(size_t(m.cap + 1) * m.kwords, 0);
       m.state.assign(size_t(m.cap) + 1, 0);
       break;
-    default:
-      return fail(vm, XE_ERR_MAPTYPE, "map type not yet implemented on the device");
+    case XE_MAP_LRU_HASH: case XE_MAP_LRU_PERCPU_HASH:
+      if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
+      m.dkind = XE_DM_LRU;
+      m.cap = next_pow2(uint64_t(def->max_entries) * 2);
+      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 2M)");
+      m.kwords = (def->key_size + 7) / 8;
+      break;
+    case XE_MAP_QUEUE: case XE_MAP_STACK:
+      m.dkind = XE_DM_LIST;
+      m.stack = def->type == XE_MAP_STACK;
+      break;
+    case XE_MAP_PERF_EVENT_ARRAY:
+      m.dkind = XE_DM_PERF;
+      break;
+    default:  // AbstractMapToVM, emulator/maps.go:155
+      return fail(vm, XE_ERR_MAPTYPE, "map type not yet implemented");
   }
   m.vals_alloc = std::max<uint64_t>(8, (m.vals_bytes + 7) & ~uint64_t(7));
   m.vals.assign(m.vals_alloc, 0);
@@ -719,6 +986,27 @@ int xe_map_lookup(xe_vm* vm, int32_t mi, const void* key, void* value) {
   if (!m || !key) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->ordered()) {
+    const HostMap::Rec* r = nullptr;
+    if (m->dkind == XE_DM_LRU) {  // userspace Lookup promotes too (maps_hash_lru.go:70-91)
+      const size_t i = lru_index(*m, std::vector<uint8_t>((const uint8_t*)key, (const uint8_t*)key + m->def.key_size));
+      if (i == m->items.size()) return 0;
+      lru_promote_host(*m, i);
+      m->host_dirty = true;
+      r = &m->items[0];
+    } else {  // QUEUE / STACK / PERF by index (maps_queue.go:39-58, maps_stack.go:38-58, maps_perf_event_array.go:45-65)
+      uint32_t kv;
+      memcpy(&kv, key, 4);
+      if (kv >= m->items.size()) return 0;
+      r = &m->items[m->dkind == XE_DM_LIST && m->stack ? m->items.size() - 1 - kv : kv];
+    }
+    if (value) {
+      const size_t n = m->dkind == XE_DM_PERF ? r->val.size() : m->def.value_size;
+      memset(value, 0, n);
+      memcpy(value, r->val.data(), std::min(n, r->val.size()));
+    }
+    return 1;
+  }
   if (m->dkind == XE_DM_ARRAY) {
     uint32_t kv; memcpy(&kv, key, 4);
     if (kv >= m->def.max_entries) return 0;
@@ -741,6 +1029,25 @@ int xe_map_update(xe_vm* vm, int32_t mi, const void* key, const void* value) {
   if (!m || !key || !value) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_LRU) {  // HashMapLRU.Update, maps_hash_lru.go:93-161
+    std::vector<uint8_t> k((const uint8_t*)key, (const uint8_t*)key + m->def.key_size);
+    size_t i = lru_index(*m, k);
+    if (i == m->items.size()) {
+      if (m->items.size() + 1 > m->def.max_entries) {
+        if (m->items.empty()) return fail(vm, XE_ERR_NOMEM, "map is full");
+        m->items.pop_back();  // evict the least recently used
+      }
+      HostMap::Rec r;
+      r.key = k;
+      m->items.push_back(std::move(r));
+      i = m->items.size() - 1;
+    }
+    m->items[i].val.assign((const uint8_t*)value, (const uint8_t*)value + m->def.value_size);
+    lru_promote_host(*m, i);
+    m->host_dirty = true;
+    return XE_OK;
+  }
+  if (m->ordered()) return fail(vm, XE_ERR_INVAL, "update not available on this map type");
   if (m->dkind == XE_DM_ARRAY) {
     uint32_t kv; memcpy(&kv, key, 4);
     if (kv >= m->def.max_entries) return fail(vm, XE_ERR_INVAL, "key out of range");
@@ -771,9 +1078,17 @@ int xe_map_update_batch(xe_vm* vm, int32_t mi, const void* keys, const void* val
 
 int xe_map_delete(xe_vm* vm, int32_t mi, const void* key) {
   HostMap* m = get_map(vm, mi);
-  if (!m || !key || m->dkind != XE_DM_HASH) return XE_ERR_INVAL;
+  if (!m || !key || (m->dkind != XE_DM_HASH && m->dkind != XE_DM_LRU)) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_LRU) {  // delete, maps_hash_lru.go:163-183
+    const size_t i = lru_index(*m, std::vector<uint8_t>((const uint8_t*)key, (const uint8_t*)key + m->def.key_size));
+    if (i < m->items.size()) {
+      m->items.erase(m->items.begin() + long(i));
+      m->host_dirty = true;
+    }
+    return XE_OK;
+  }
   uint64_t kw[XE_MAX_KEY / 8];
   m->pack_key(key, kw);
   int64_t s = m->find(kw);
@@ -790,7 +1105,7 @@ int xe_map_count(xe_vm* vm, int32_t mi, uint64_t* count) {
   if (!m || !count) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
-  *count = m->dkind == XE_DM_ARRAY ? m->def.max_entries : m->count;
+  *count = m->dkind == XE_DM_ARRAY ? m->def.max_entries : m->ordered() ? m->items.size() : m->count;
   return XE_OK;
 }
 
@@ -799,6 +1114,37 @@ int xe_map_dump(xe_vm* vm, int32_t mi, void* keys_or_raw, void* values, uint64_t
   if (!m) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (m->dkind == XE_DM_LRU) {  // MA6: (key, value) sorted by key bytes, the nil key first
+    if (count) *count = m->items.size();
+    if (!keys_or_raw && !values) return XE_OK;
+    if (cap < m->items.size()) return fail(vm, XE_ERR_INVAL, "dump buffer too small");
+    std::vector<size_t> order(m->items.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+      const auto& x = m->items[a];
+      const auto& y = m->items[b];
+      if (x.nil_key || y.nil_key) return x.nil_key && !y.nil_key;
+      return x.key < y.key;
+    });
+    for (size_t j = 0; j < order.size(); j++) {
+      const auto& r = m->items[order[j]];
+      if (keys_or_raw) {
+        uint8_t* kd = (uint8_t*)keys_or_raw + j * m->def.key_size;
+        memset(kd, 0, m->def.key_size);
+        if (!r.nil_key) memcpy(kd, r.key.data(), m->def.key_size);
+      }
+      if (values) {
+        uint8_t* vd = (uint8_t*)values + j * m->def.value_size;
+        memset(vd, 0, m->def.value_size);
+        memcpy(vd, r.val.data(), std::min<size_t>(r.val.size(), m->def.value_size));
+      }
+    }
+    return XE_OK;
+  }
+  if (m->ordered()) {  // QUEUE / STACK / PERF: xe_map_dump_list
+    if (count) *count = m->items.size();
+    return XE_OK;
+  }
   if (m->dkind == XE_DM_ARRAY) {
     if (count) *count = m->def.max_entries;
     if (keys_or_raw && cap >= m->def.max_entries) memcpy(keys_or_raw, m->vals.data(), m->vals_bytes);
@@ -898,6 +1244,55 @@ static bool may_write_packet(const std::vector<XeUop>& prog) {
   return true;
 }
 
+// Can the program run as a per-program kernel? Not with bpf-to-bpf calls or tail calls (the frames,
+// clones and program switches live in the interpreter's general model), the ordered maps, or helpers
+// whose id is only known at run time.
+static bool jit_possible(const xe_vm* vm) {
+  for (const XeUop& u : vm->programs[vm->entry]) {
+    if (u.cls == U_CALLBPF || u.cls == U_CALLX) return false;
+    if (u.cls == U_HELPER && (u.imm == 12 || u.imm == 25 || u.imm == 87 || u.imm == 88 || u.imm == 89)) return false;
+  }
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].ordered()) return false;
+  return true;
+}
+static bool has_callbpf(const xe_vm* vm) {
+  for (size_t p = 1; p < vm->programs.size(); p++)
+    for (const XeUop& u : vm->programs[p])
+      if (u.cls == U_CALLBPF) return true;
+  return false;
+}
+static bool has_ordered_maps(const xe_vm* vm) {
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].ordered()) return true;
+  return false;
+}
+
+// arena for `nl` lanes: parallel capacities are modest (a lane that runs out raises XE_FLAG_CAPACITY
+// and the batch is replayed in order), the ordered replay's single lane gets x seq_scale more
+static int ensure_arena(xe_vm* vm, bool seq, uint32_t nl, XeGen& g) {
+  const bool calls = has_callbpf(vm);
+  const uint32_t k = seq ? vm->seq_scale : 1u;
+  const uint32_t nobj = seq ? 65536u * k : 256u;
+  const uint32_t nframes = calls ? 8u : 1u;
+  const uint32_t nvc = calls ? (seq ? 4096u * k : 16u) : 0u;
+  const uint32_t nbm = calls ? (seq ? 4096u * k : 16u) : 0u;
+  const uint64_t nbytes = calls ? (seq ? (uint64_t(64) << 20) * k : 4096u) : 0u;
+  uint64_t total = 0;
+  g = gen_layout(nl, nobj, nframes, nvc, nbm, nbytes, &total);
+  uint8_t*& buf = seq ? vm->d_arena_seq : vm->d_arena_par;
+  uint64_t& have = seq ? vm->arena_seq_bytes : vm->arena_par_bytes;
+  if (!buf || have < total) {
+    dev_free(buf);
+    buf = nullptr;
+    have = 0;
+    if (dev_alloc((void**)&buf, size_t(total))) return -1;
+    have = total;
+  }
+  g.base = buf;
+  return 0;
+}
+
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
@@ -907,7 +1302,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
 
   XeParams P{};
-  P.prog = vm->d_prog;
+  P.progs = vm->d_progs;
+  P.prog_off = vm->d_prog_off;
+  P.prog_lens = vm->d_prog_off + vm->d_progs_n + 1;
+  P.nprogs = uint32_t(vm->d_progs_n);
+  P.entry = vm->entry;
+  P.prog = vm->d_progs + vm->prog_off[size_t(vm->entry)];
   P.prog_len = int32_t(vm->d_prog_len);
   P.umem = (uint8_t*)d_umem;
   P.umem_len = umem_len;
@@ -928,27 +1328,32 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
 
   const uint32_t mode = vm->settings.mode;
-  uint32_t engine = vm->settings.engine;
-  if (const char* env = getenv("XE_ENGINE")) engine = !strcmp(env, "interp") ? XE_ENGINE_INTERP : !strcmp(env, "jit") ? XE_ENGINE_JIT : engine;
+  const uint32_t engine = vm->settings.engine;
   void* jit = nullptr;
+  bool jit_general = false;
 #ifndef XE_HOSTSIM
-  if (engine != XE_ENGINE_INTERP) {
+  if (engine != XE_ENGINE_INTERP && jit_possible(vm)) {
     if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size()) {
       // the kernel is specialised on the program and the map geometry (xe_jit.cpp)
       const auto& prog = vm->programs[vm->entry];
       const char* jerr = "";
       vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
-                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &jerr);
+                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &vm->jit_general, &jerr);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
       vm->jit_nmaps = vm->maps.size();
     }
     jit = vm->jit_fn;
+    jit_general = vm->jit_general;
     // acyclic kernels carry no budget checks: exact only while the budget cannot be reached
     if (jit && !vm->jit_cyclic && vm->settings.max_steps < vm->d_prog_len) jit = nullptr;
-    if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
+  } else if (engine == XE_ENGINE_JIT) {
+    vm->jit_error = "the program needs the interpreter's general model (bpf-to-bpf or tail calls, ordered maps, "
+                    "indirect helper calls)";
   }
+  if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
 #endif
+  const bool general = !jit || jit_general;  // lanes keep their state in the XeGen arena
   auto launch = [&](const XeParams* p, uint32_t b, uint32_t t) {
     return jit ? launch_jit(jit, p, b, t, s) : launch_interp(p, b, t, s);
   };
@@ -960,6 +1365,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     std::vector<uint64_t> words;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
+      if (m.ordered()) continue;
       src.push_back(m.d_vals);
       dst.push_back(m.d_snap);
       words.push_back(m.vals_alloc / 8);
@@ -971,13 +1377,91 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   const bool keep_pkts = mode == XE_MODE_AUTO && umem_len && may_write_packet(vm->programs[vm->entry]);
   if (keep_pkts && (ensure_buf(&vm->d_usnap, &vm->d_usnap_cap, umem_len) || d2d(vm->d_usnap, d_umem, umem_len, s)))
     return fail(vm, XE_ERR_DEVICE, "packet snapshot");
+  std::vector<unsigned long long> aux(aux_used);
+  std::vector<unsigned long long> red;
+  // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
+  auto reduce = [&]() {
+    red.assign(16 + 2 * size_t(P.nmaps + 1), 0);
+    red[0] = aux[0];
+    for (uint32_t r = 0; r < kRep; r++) {
+      const unsigned long long* rec = aux.data() + 16 + size_t(r) * P.rep_words;
+      red[1] += rec[0];
+      for (int k = 0; k < 8; k++) red[2 + k] += rec[1 + k];
+      for (int k = 0; k < 4; k++) red[XE_REC_WIDTH0 + 2 + k] |= rec[XE_REC_WIDTH0 + k];
+      for (uint32_t w = 0; w < 2 * (P.nmaps + 1); w++) red[16 + w] |= rec[16 + w];
+    }
+  };
+  auto read_aux = [&]() -> int {
+    if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return -1;
+    reduce();
+    return 0;
+  };
+  // roll maps and packets back to the run's start
+  auto rollback = [&](bool hash_records) -> int {
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (!m.ordered() && d2d(m.d_vals, m.d_snap, m.vals_alloc, s)) return -1;
+    }
+    if (hash_records) {
+      uint64_t off = 0;
+      for (size_t i = 1; i < vm->maps.size(); i++) {
+        HostMap& m = vm->maps[i];
+        if (m.dkind != XE_DM_HASH) continue;
+        const uint64_t rb = uint64_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8;
+        if (d2d(m.d_keys, (uint8_t*)vm->d_ksnap + off, rb, s) || d2d(m.d_count, (uint8_t*)vm->d_ksnap + off + rb, 4, s)) return -1;
+        off += rb + 8;
+      }
+      for (size_t i = 1; i < vm->maps.size(); i++)  // the ordered maps come back from the host mirror
+        if (vm->maps[i].ordered() && ordered_upload(vm, vm->maps[i], vm->ord_slack, vm->ord_slack_bytes)) return -1;
+    }
+    if (keep_pkts && d2d(d_umem, vm->d_usnap, umem_len, s)) return -1;
+    return dmemset(vm->d_aux, 0, aux_used * 8, s);
+  };
+  // The exact ordered replay: one lane walks the packets in order. Its arena (and the ordered maps'
+  // room) grows x4 and the replay restarts from the rollback point whenever it runs out.
+  auto sequential = [&](float& ms) -> int {
+    // rollback point of what the parallel pass never writes: hash slot records, the ordered maps
+    uint64_t kb = 0;
+    for (size_t i = 1; i < vm->maps.size(); i++)
+      if (vm->maps[i].dkind == XE_DM_HASH) kb += uint64_t(vm->maps[i].cap + 1) * xe_hash_rwords(vm->maps[i].kwords) * 8 + 8;
+    if (kb && ensure_buf((void**)&vm->d_ksnap, &vm->d_ksnap_bytes, kb)) return fail(vm, XE_ERR_DEVICE, "device alloc (snapshot)");
+    uint64_t off = 0;
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (m.dkind == XE_DM_HASH) {
+        const uint64_t rb = uint64_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8;
+        if (d2d((uint8_t*)vm->d_ksnap + off, m.d_keys, rb, s) || d2d((uint8_t*)vm->d_ksnap + off + rb, m.d_count, 4, s))
+          return fail(vm, XE_ERR_DEVICE, "snapshot");
+        off += rb + 8;
+      }
+      if (m.ordered() && map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
+    }
+    for (int attempt = 0;; attempt++) {
+      P.mode = XE_MODE_SEQUENTIAL;
+      if (general && ensure_arena(vm, true, 1, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (replay arena)");
+      vm->t1.rec(s);
+      if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+      vm->t2.rec(s);
+      if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+      ms += Timer::ms(vm->t1, vm->t2);
+      if (!(red[0] & XE_FLAG_CAPACITY)) return XE_OK;
+      if (attempt >= 6) return fail(vm, XE_ERR_NOMEM, "the ordered replay outgrew its device arena");
+      vm->seq_scale *= 4;
+      vm->ord_slack *= 4;
+      vm->ord_slack_bytes *= 4;
+      if (rollback(true) || prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      P.maps = vm->d_maps;
+    }
+  };
+
   vm->t0.rec(s);
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
-  if (mode == XE_MODE_SEQUENTIAL) {
-    P.mode = XE_MODE_SEQUENTIAL;
+  float kms = 0;
+  if (mode == XE_MODE_SEQUENTIAL || (mode == XE_MODE_AUTO && has_ordered_maps(vm))) {
+    // ordered maps: every operation on them is order-dependent; replay straight away
     used = XE_MODE_SEQUENTIAL;
-    if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    if (int rc = sequential(kms)) return rc;
   } else {
     P.mode = XE_MODE_PARALLEL;
     if (vm->cus < 0) vm->cus = cu_count(vm->settings.device);
@@ -989,59 +1473,33 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     }
     if (occ < 0) occ = blocks_per_cu(jit, P.nmaps);
     vm->last_grid = grid_blocks(n, occ, vm->cus);
+    if (general) {
+      vm->last_grid = std::min<uint32_t>(vm->last_grid, 512);  // bounds the per-lane arena
+      if (ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+    }
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
-  }
-  vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
-  if (mode != XE_MODE_SEQUENTIAL) {
+    vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
     // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
       if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
         return fail(vm, XE_ERR_DEVICE, "replica fold");
     }
-  }
-  std::vector<unsigned long long> aux(aux_used);
-  // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
-  auto reduce = [&](std::vector<unsigned long long>& sum) {
-    sum.assign(16 + 2 * size_t(P.nmaps + 1), 0);
-    sum[0] = aux[0];
-    for (uint32_t r = 0; r < kRep; r++) {
-      const unsigned long long* rec = aux.data() + 16 + size_t(r) * P.rep_words;
-      sum[1] += rec[0];
-      for (int k = 0; k < 8; k++) sum[2 + k] += rec[1 + k];
-      for (int k = 0; k < 4; k++) sum[XE_REC_WIDTH0 + 2 + k] |= rec[XE_REC_WIDTH0 + k];
-      for (uint32_t w = 0; w < 2 * (P.nmaps + 1); w++) sum[16 + w] |= rec[16 + w];
-    }
-  };
-  std::vector<unsigned long long> red;
-  if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
-  reduce(red);
-  float kms = Timer::ms(vm->t0, vm->t1);
-  if (mode != XE_MODE_SEQUENTIAL) {
-    uint32_t flags = uint32_t(red[0]);
-    conflict = (flags & XE_FLAG_ORDERED) != 0;
+    if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+    kms = Timer::ms(vm->t0, vm->t1);
+    const uint32_t flags = uint32_t(red[0]);
+    conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
     for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
       if (red[16 + 2 * m] & red[16 + 2 * m + 1]) conflict = true;
       // atomic adds of more than one width on a map do not commute (carry stops at a field's top)
       const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
       if (wc & (wc - 1)) conflict = true;
     }
-    if (conflict && mode == XE_MODE_AUTO) {
-      // order-dependent batch: roll the maps back and replay it in packet order on one lane
-      for (size_t i = 1; i < vm->maps.size(); i++) {
-        HostMap& m = vm->maps[i];
-        if (d2d(m.d_vals, m.d_snap, m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
-      }
-      if (keep_pkts && d2d(d_umem, vm->d_usnap, umem_len, s)) return fail(vm, XE_ERR_DEVICE, "packet rollback");
-      if (dmemset(vm->d_aux, 0, aux_used * 8, s)) return fail(vm, XE_ERR_DEVICE, "memset");
-      P.mode = XE_MODE_SEQUENTIAL;
+    if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
+      // order-dependent batch (or a lane out of arena): roll the maps back and replay in packet order
+      if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
       used = XE_MODE_SEQUENTIAL;
-      vm->t1.rec(s);
-      if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
-      vm->t2.rec(s);
-      if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "kernel failed");
-      reduce(red);
-      kms += Timer::ms(vm->t1, vm->t2);
+      if (int rc = sequential(kms)) return rc;
     }
   }
   for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
@@ -1102,6 +1560,55 @@ int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc
   if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
   if (stats) stats->total_ms = Timer::ms(a, b);
   a.fini(); b.fini();
+  return XE_OK;
+}
+
+int xe_map_dump_list(xe_vm* vm, int32_t mi, void* data, uint64_t data_cap, uint32_t* lens, uint64_t cap, uint64_t* count,
+                     uint64_t* bytes) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || (m->dkind != XE_DM_LIST && m->dkind != XE_DM_PERF)) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  uint64_t total = 0;
+  for (auto& r : m->items) total += r.val.size();
+  if (count) *count = m->items.size();
+  if (bytes) *bytes = total;
+  if (!data && !lens) return XE_OK;
+  if (cap < m->items.size() || (data && data_cap < total)) return fail(vm, XE_ERR_INVAL, "dump buffer too small");
+  uint64_t off = 0;
+  for (size_t i = 0; i < m->items.size(); i++) {
+    if (lens) lens[i] = uint32_t(m->items[i].val.size());
+    if (data && !m->items[i].val.empty()) memcpy((uint8_t*)data + off, m->items[i].val.data(), m->items[i].val.size());
+    off += m->items[i].val.size();
+  }
+  return XE_OK;
+}
+
+int xe_map_lru_order(xe_vm* vm, int32_t mi, void* keys, uint64_t cap, uint64_t* count) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || m->dkind != XE_DM_LRU) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  if (count) *count = m->items.size();
+  if (!keys) return XE_OK;
+  if (cap < m->items.size()) return fail(vm, XE_ERR_INVAL, "buffer too small");
+  for (size_t i = 0; i < m->items.size(); i++) {
+    uint8_t* kd = (uint8_t*)keys + i * m->def.key_size;
+    memset(kd, 0, m->def.key_size);
+    if (!m->items[i].nil_key) memcpy(kd, m->items[i].key.data(), m->def.key_size);
+  }
+  return XE_OK;
+}
+
+int xe_map_push(xe_vm* vm, int32_t mi, const void* value) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !value || m->dkind != XE_DM_LIST) return XE_ERR_INVAL;
+  set_device(vm->settings.device);
+  if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+  HostMap::Rec r;
+  r.val.assign((const uint8_t*)value, (const uint8_t*)value + m->def.value_size);
+  m->items.push_back(std::move(r));
+  m->host_dirty = true;
   return XE_OK;
 }
 

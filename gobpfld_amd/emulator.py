@@ -20,8 +20,12 @@ import numpy as np
 
 from . import _native as N
 
-STATUS = {0: "OK", 1: "VMERR", 2: "PANIC", 3: "BUDGET", 4: "UNSUPPORTED", 5: "CAPACITY"}
+STATUS = {0: "OK", 1: "VMERR", 2: "PANIC", 3: "BUDGET", 4: "UNSUPPORTED"}
 MAP_HASH, MAP_ARRAY, MAP_PROG_ARRAY, MAP_PERF_EVENT_ARRAY, MAP_PERCPU_HASH, MAP_PERCPU_ARRAY = 1, 2, 3, 4, 5, 6
+MAP_LRU_HASH, MAP_LRU_PERCPU_HASH, MAP_ARRAY_OF_MAPS, MAP_HASH_OF_MAPS, MAP_QUEUE, MAP_STACK = 9, 10, 12, 13, 22, 23
+ARRAY_TYPES = (MAP_ARRAY, MAP_PERCPU_ARRAY, MAP_PROG_ARRAY, MAP_ARRAY_OF_MAPS)
+HASH_TYPES = (MAP_HASH, MAP_PERCPU_HASH, MAP_HASH_OF_MAPS, MAP_LRU_HASH, MAP_LRU_PERCPU_HASH)
+LIST_TYPES = (MAP_QUEUE, MAP_STACK, MAP_PERF_EVENT_ARRAY)
 MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL = 0, 1, 2
 ENGINE_AUTO, ENGINE_INTERP, ENGINE_JIT = 0, 1, 2
 
@@ -155,7 +159,7 @@ class VM:
     def map_update_batch(self, m: int, keys: np.ndarray, values: np.ndarray) -> None:
         """Bulk update: keys (n, key_size) and values (n, value_size) uint8 arrays."""
         d = self.map_defs[m]
-        ks = d.key_size if d.type in (MAP_HASH, MAP_PERCPU_HASH, 13) else 4
+        ks = d.key_size if d.type in HASH_TYPES else 4
         k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, ks)
         v = np.ascontiguousarray(values, dtype=np.uint8).reshape(-1, d.value_size)
         assert len(k) == len(v)
@@ -174,12 +178,15 @@ class VM:
         self._check(self.lib.map_delete(self.h, m, bytes(key).ljust(max(d.key_size, 4), b"\0")), "map delete")
 
     def map_dump(self, m: int):
-        """ARRAY -> raw bytes (ValueSize*MaxEntries); HASH -> (keys[n,ks], values[n,vs]) sorted by key."""
+        """ARRAY -> raw bytes (ValueSize*MaxEntries); HASH / LRU_HASH -> (keys[n,ks], values[n,vs]) sorted
+        by key; QUEUE / STACK / PERF_EVENT_ARRAY -> list of records (bytes) in list order."""
         d = self.map_defs[m]
+        if d.type in LIST_TYPES:
+            return self.map_dump_list(m)
         cnt = C.c_uint64()
         self._check(self.lib.map_dump(self.h, m, None, None, 0, C.byref(cnt)), "map dump")
         n = cnt.value
-        if d.type in (MAP_ARRAY, MAP_PERCPU_ARRAY, MAP_PROG_ARRAY, 12):
+        if d.type in ARRAY_TYPES:
             raw = np.zeros(d.value_size * d.max_entries, dtype=np.uint8)
             self._check(self.lib.map_dump(self.h, m, raw.ctypes.data, None, n, C.byref(cnt)), "map dump")
             return raw.tobytes()
@@ -188,6 +195,34 @@ class VM:
         self._check(self.lib.map_dump(self.h, m, keys.ctypes.data if n else None,
                                       vals.ctypes.data if n else None, n, C.byref(cnt)), "map dump")
         return keys, vals
+
+    def map_dump_list(self, m: int) -> list[bytes]:
+        """QUEUE / STACK / PERF_EVENT_ARRAY records in the order of the Go Values / Events slice."""
+        cnt, nb = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.map_dump_list(self.h, m, None, 0, None, 0, C.byref(cnt), C.byref(nb)), "map dump list")
+        data = np.zeros(max(1, nb.value), dtype=np.uint8)
+        lens = np.zeros(max(1, cnt.value), dtype=np.uint32)
+        self._check(self.lib.map_dump_list(self.h, m, data.ctypes.data, nb.value, lens.ctypes.data, cnt.value,
+                                           C.byref(cnt), C.byref(nb)), "map dump list")
+        out, off = [], 0
+        for ln in lens[: cnt.value]:
+            out.append(data[off: off + int(ln)].tobytes())
+            off += int(ln)
+        return out
+
+    def map_lru_order(self, m: int) -> list[bytes]:
+        """LRU_HASH UsageList keys, most recently used first (maps_hash_lru.go:21-24)."""
+        d = self.map_defs[m]
+        cnt = C.c_uint64()
+        self._check(self.lib.map_lru_order(self.h, m, None, 0, C.byref(cnt)), "map lru order")
+        keys = np.zeros((max(1, cnt.value), d.key_size), dtype=np.uint8)
+        self._check(self.lib.map_lru_order(self.h, m, keys.ctypes.data, cnt.value, C.byref(cnt)), "map lru order")
+        return [keys[i].tobytes() for i in range(cnt.value)]
+
+    def map_push(self, m: int, value: bytes) -> None:
+        """QueueMap/StackMap.Push of one value_size element from userspace."""
+        d = self.map_defs[m]
+        self._check(self.lib.map_push(self.h, m, bytes(value).ljust(d.value_size, b"\0")), "map push")
 
     def map_values_bytes(self, m: int) -> int:
         b = C.c_uint64()

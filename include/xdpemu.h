@@ -53,8 +53,7 @@ extern "C" {
 #define XE_ST_VMERR 1       /* Run() returned a *VMError (emulator/vm.go:175-180)                  */
 #define XE_ST_PANIC 2       /* the Go VM would panic (runtime error not recovered anywhere)        */
 #define XE_ST_BUDGET 3      /* step budget exhausted (the Go VM has none and would hang)           */
-#define XE_ST_UNSUPPORTED 4 /* feature outside this build's scope (tail call, perf output, ...)    */
-#define XE_ST_CAPACITY 5    /* device per-lane object table overflowed (device-only; see DESIGN)   */
+#define XE_ST_UNSUPPORTED 4 /* reserved: no instruction or helper of the reference reports it      */
 
 /* VMERR codes (xe_result.code when status == XE_ST_VMERR). Errors raised inside a helper
  * (emulator/inst_call_helper.go:30-33) carry XE_E_IN_HELPER in addition. */
@@ -73,7 +72,9 @@ extern "C" {
 #define XE_E_NO_HELPER 13   /* emulator/inst_call_helper.go:21-28,55-63 */
 #define XE_E_NO_MAP 14      /* emulator/inst_load.go:39-41 */
 #define XE_E_MAP_NOT_PTR 15 /* emulator/inst_load.go:49-52 */
-#define XE_E_MAP_OP 16      /* map Lookup/Update returned an error the helper does not map to errno */
+#define XE_E_MAP_OP 16      /* map Lookup/Update/Push/Pop returned an error the helper does not map to
+                             * errno, e.g. "update not available on this map type" (maps.go:61-82),
+                             * "lookup didn't return a pointer" (helper_functions.go:178-181) */
 #define XE_E_IN_HELPER 0x80
 
 /* PANIC codes (xe_result.code when status == XE_ST_PANIC) */
@@ -82,18 +83,22 @@ extern "C" {
 #define XE_P_DIV0 3      /* int32 divide by zero after a non-zero 64-bit check, emulator/inst_div.go:96 */
 #define XE_P_INDEX 4     /* index/slice out of range (negative PC, negative helper id, ReadRange) */
 #define XE_P_NIL_MAP 5   /* vm.Maps[0] == nil used as a map, emulator/inst_load.go:43-44 */
+#define XE_P_MAKESLICE 6 /* make([]byte, negative) in ReadRange, e.g. bpf_perf_event_output size < 0 */
 
 /* register kinds (emulator/registers.go:176-324) */
 #define XE_KIND_IMM 0
 #define XE_KIND_MEMPTR 1
 #define XE_KIND_FRAMEPTR 2
+#define XE_KIND_NIL 3 /* nil RegisterValue: R2 after bpf_map_peek_elem on an empty map (helper_functions.go:356-371) */
 
 /* memory regions a pointer can refer to (parity records) */
 #define XE_REGION_PACKET 0
 #define XE_REGION_CTX 1
 #define XE_REGION_STACK 2
 #define XE_REGION_ARRAY 3
-#define XE_REGION_HASHVAL 4
+#define XE_REGION_HASHVAL 4  /* HASH and LRU_HASH values */
+#define XE_REGION_QUEUEVAL 5 /* QUEUE / STACK elements */
+#define XE_REGION_PERF 6     /* PERF_EVENT_ARRAY events (Lookup shares the event bytes) */
 
 /* map types: numeric values of bpftypes.BPFMapType (bpftypes/bpf_types.go:155-277) */
 #define XE_MAP_HASH 1
@@ -213,6 +218,19 @@ int xe_map_update_batch(xe_vm* vm, int32_t map_idx, const void* keys, const void
 int xe_map_count(xe_vm* vm, int32_t map_idx, uint64_t* count);
 int xe_map_dump(xe_vm* vm, int32_t map_idx, void* keys_or_raw, void* values, uint64_t cap_entries,
                 uint64_t* count);
+
+/* Ordered maps (LRU_HASH, QUEUE, STACK, PERF_EVENT_ARRAY; emulator/maps_hash_lru.go, maps_queue.go,
+ * maps_stack.go, maps_perf_event_array.go). xe_map_lookup on an LRU_HASH promotes the key as the Go
+ * Lookup does; on a QUEUE / STACK / PERF_EVENT_ARRAY the key is a u32 index into the list.
+ * QUEUE / STACK / PERF_EVENT_ARRAY contents in Go slice order (queue front first, stack bottom first,
+ * events oldest first): `data` receives the records back to back, `lens` their lengths (0 for a nil
+ * backing). NULL buffers query *count and *bytes. */
+int xe_map_dump_list(xe_vm* vm, int32_t map_idx, void* data, uint64_t data_cap, uint32_t* lens, uint64_t cap,
+                     uint64_t* count, uint64_t* bytes);
+/* LRU_HASH UsageList (maps_hash_lru.go:21-24): keys, most recently used first, key_size bytes each */
+int xe_map_lru_order(xe_vm* vm, int32_t map_idx, void* keys, uint64_t cap, uint64_t* count);
+/* QueueMap/StackMap.Push from userspace (maps_queue.go:60-77): one value_size element */
+int xe_map_push(xe_vm* vm, int32_t map_idx, const void* value);
 
 /* --- running: the per-packet harness of SURVEY Appendix B over a batch ---
  * Each packet i runs Reset; R1 = &MemoryPtr{ctx}; Run (emulator/vm.go:110-173, 211-246).

@@ -335,6 +335,11 @@ struct Memory {  // emulator/memory.go:11-18
 };
 
 static inline int64_t wadd(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
+
+// A RegisterValue interface may be nil: bpf_map_peek_elem on an empty queue/stack sets R2 = nil
+// (helper_functions.go:356-371). Calling a method on it panics; a type assertion on it fails.
+static int64_t V(const RV* r) { if (!r) throw GoPanic{XE_P_NIL_DEREF}; return r->Value(); }
+static int KindOf(const RV* r) { if (!r) throw GoPanic{XE_P_NIL_DEREF}; return r->kind(); }
 static inline int64_t wmul(int64_t a, int64_t b) { return int64_t(uint64_t(a) * uint64_t(b)); }
 
 // Go bounds check `offset < 0 || offset+size > len` with wrapping addition; an index that passes
@@ -360,6 +365,7 @@ struct ValueMemory : Memory {  // emulator/memory.go:23-120
   }
   int ReadRange(int64_t off, int64_t count, std::vector<uint8_t>* out) override {  // memory.go:55-95
     if (off < 0 || wadd(off, count) > Size()) return XE_E_OOB;
+    if (count < 0) throw GoPanic{XE_P_MAKESLICE};  // make([]byte, count)
     std::vector<uint8_t> r(size_t(count), 0);
     for (int64_t i = 0; i < count;) {
       RV* v = mapping[off + i];
@@ -395,6 +401,7 @@ struct ByteMemory : Memory {  // emulator/memory.go:125-223 (little endian; Byte
   int Read(int64_t off, int size, RV** out, VM* vm) override;
   int ReadRange(int64_t off, int64_t count, std::vector<uint8_t>* out) override {  // memory.go:176-185
     if (off < 0 || wadd(off, count) > len) return XE_E_OOB;
+    if (count < 0) throw GoPanic{XE_P_MAKESLICE};
     out->assign(data() + off, data() + off + count);
     return 0;
   }
@@ -410,13 +417,17 @@ struct ByteMemory : Memory {  // emulator/memory.go:125-223 (little endian; Byte
 
 // ---------------------------------------------------------------- maps
 enum MapErr { ME_OK = 0, ME_KEY_NO_PTR = 1, ME_VAL_NO_PTR = 2, ME_OOM = 3, ME_NOT_IMPL = 4 };
+constexpr int ME_GENERIC = 0x100 | XE_E_MAP_OP;  // a non-sentinel error: the helper aborts the VM
 struct Map {
   xe_map_def def{};
   int index = 0;
   virtual ~Map() {}
   // return ME_* or (0x100 | memory error code) for a generic error that aborts the VM
   virtual int Lookup(VM* vm, RV* key, RV** out) = 0;
-  virtual int Update(VM* vm, RV* key, RV* value, RV** out) = 0;
+  // AbstractMap defaults (emulator/maps.go:61-82): "... not available on this map type"
+  virtual int Update(VM*, RV*, RV*, RV**) { return ME_GENERIC; }
+  virtual int Push(VM*, RV*, int64_t) { return ME_GENERIC; }
+  virtual int Pop(VM*, RV**) { return ME_GENERIC; }
   virtual bool isHash() const { return false; }
 };
 
@@ -426,6 +437,7 @@ struct VM {
   FramePtr* R10 = nullptr;
   int64_t PC = 0;
   int PI = 0;
+  int entry = 0;  // SetEntrypoint's index: the harness starts every packet there
   std::vector<ValueMemory> frames;
   struct Preserved { int64_t PC; RV* R[4]; };
   std::vector<Preserved> preserved;
@@ -467,7 +479,7 @@ Memory* ByteMemory::Clone(VM* vm) {  // memory.go:212-219: copies the bytes
 
 // RegisterValue.Copy (registers.go:186-188, 222-227, 283-292): FramePointer copies are writable.
 static RV* copyRV(VM* vm, RV* r) {
-  switch (r->kind()) {
+  switch (KindOf(r)) {
     case XE_KIND_IMM: return vm->newIMM(r->Value());
     case XE_KIND_MEMPTR: { auto* p = static_cast<MemPtr*>(r); return vm->mk<MemPtr>(p->mem, p->off); }
     default: { auto* p = static_cast<FramePtr*>(r); return vm->mk<FramePtr>(p->mem, p->index, p->off, false); }
@@ -475,7 +487,7 @@ static RV* copyRV(VM* vm, RV* r) {
 }
 // RegisterValue.Clone (registers.go:190-192, 229-240, 294-303): deep-copies the memory.
 static RV* cloneRV(VM* vm, RV* r) {
-  switch (r->kind()) {
+  switch (KindOf(r)) {
     case XE_KIND_IMM: return vm->newIMM(r->Value());
     case XE_KIND_MEMPTR: { auto* p = static_cast<MemPtr*>(r); return vm->mk<MemPtr>(p->mem->Clone(vm), p->off); }
     default: { auto* p = static_cast<FramePtr*>(r); return vm->mk<FramePtr>(p->mem->Clone(vm), p->index, p->off, p->ro); }
@@ -483,7 +495,7 @@ static RV* cloneRV(VM* vm, RV* r) {
 }
 // RegisterValue.Assign (registers.go:194-197, 243-247, 305-313)
 static int assignRV(RV* r, int64_t v) {
-  switch (r->kind()) {
+  switch (KindOf(r)) {
     case XE_KIND_IMM: static_cast<IMM*>(r)->v = v; return 0;
     case XE_KIND_MEMPTR: static_cast<MemPtr*>(r)->off = v; return 0;
     default: {
@@ -494,7 +506,8 @@ static int assignRV(RV* r, int64_t v) {
     }
   }
 }
-static bool isPointer(RV* r) { return r->kind() != XE_KIND_IMM; }  // PointerValue type assertion
+static bool isPointer(RV* r) { return r && r->kind() != XE_KIND_IMM; }  // PointerValue type assertion (nil: false)
+static bool isMemPtr(RV* r) { return r && r->kind() == XE_KIND_MEMPTR; }  // *MemoryPtr type assertion
 
 // PointerValue.Deref / ReadRange (registers.go:218-220, 273-281)
 static int derefRV(VM* vm, RV* r, int64_t offset, int size, RV** out) {
@@ -528,8 +541,8 @@ struct ArrayMap : Map {  // emulator/maps_array.go
     return 0;
   }
   int Update(VM* vm, RV* key, RV* value, RV** out) override {  // maps_array.go:89-131
-    if (value->kind() != XE_KIND_MEMPTR) return ME_VAL_NO_PTR;
-    if (key->kind() != XE_KIND_MEMPTR) return ME_VAL_NO_PTR;
+    if (!isMemPtr(value)) return ME_VAL_NO_PTR;
+    if (!isMemPtr(key)) return ME_VAL_NO_PTR;
     RV* kvr = nullptr;
     if (int e = derefRV(vm, key, 0, 4, &kvr)) return 0x100 | e;
     int64_t kv = kvr->Value();
@@ -579,6 +592,139 @@ struct HashMap : Map {  // emulator/maps_hash.go; sha256(key) is unobservable, s
   }
 };
 
+// HashMapLRU, emulator/maps_hash_lru.go. Entries keyed by key bytes (sha256 is unobservable; a
+// ReadRange error gives the empty key, as `if !ok` ignores it, :76-79); UsageList holds keys, MRU first.
+struct LRUHashMap : Map {
+  std::map<std::vector<uint8_t>, std::unique_ptr<ByteMemory>> values;
+  std::vector<std::vector<uint8_t>> usage;  // UsageList
+  std::vector<std::unique_ptr<ByteMemory>> evicted;  // evicted values stay valid for pointers still held
+  bool isHash() const override { return true; }
+  std::vector<uint8_t> keyBytes(RV* key) {
+    std::vector<uint8_t> k;
+    if (readRangeRV(key, 0, def.key_size, &k) != 0) k.clear();
+    return k;
+  }
+  void promote(const std::vector<uint8_t>& key) {  // :51-68
+    size_t cur = 0;
+    for (size_t i = 0; i < usage.size(); i++)
+      if (usage[i] == key) { cur = i; break; }
+    if (cur == 0) return;
+    std::vector<uint8_t> k = usage[cur];
+    for (size_t i = cur; i > 0; i--) usage[i] = usage[i - 1];
+    usage[0] = k;
+  }
+  void erase(const std::vector<uint8_t>& key) {  // delete, :163-183
+    size_t cur = usage.size();
+    for (size_t i = 0; i < usage.size(); i++)
+      if (usage[i] == key) { cur = i; break; }
+    if (cur == usage.size()) return;
+    usage.erase(usage.begin() + long(cur));
+    auto it = values.find(key);
+    if (it != values.end()) { evicted.push_back(std::move(it->second)); values.erase(it); }
+  }
+  int Lookup(VM* vm, RV* key, RV** out) override {  // :70-91
+    if (!isPointer(key)) return ME_KEY_NO_PTR;
+    std::vector<uint8_t> kb = keyBytes(key);
+    auto it = values.find(kb);
+    if (it == values.end()) { *out = vm->newIMM(0); return 0; }
+    promote(kb);
+    *out = vm->mk<MemPtr>(it->second.get(), 0);
+    return 0;
+  }
+  int Update(VM* vm, RV* key, RV* value, RV** out) override {  // :93-161
+    if (!isPointer(key)) return ME_KEY_NO_PTR;
+    std::vector<uint8_t> kb = keyBytes(key);
+    auto it = values.find(kb);
+    const bool found = it != values.end();
+    if (!found && values.size() + 1 > def.max_entries) {
+      if (usage.empty()) throw GoPanic{XE_P_INDEX};  // UsageList[len-1] of an empty list
+      erase(std::vector<uint8_t>(usage.back()));      // evicted before the value is even checked
+    }
+    if (!isPointer(value)) return ME_VAL_NO_PTR;
+    std::vector<uint8_t> vb;
+    if (readRangeRV(value, 0, def.value_size, &vb) != 0) vb.clear();
+    if (!found) {
+      auto m = std::make_unique<ByteMemory>();
+      m->region = XE_REGION_HASHVAL; m->mapidx = index;
+      it = values.emplace(kb, std::move(m)).first;
+      usage.push_back(kb);
+    }
+    promote(kb);
+    it->second->setBacking(std::move(vb));
+    *out = vm->newIMM(0);
+    return 0;
+  }
+};
+
+// QueueMap / StackMap, emulator/maps_queue.go, emulator/maps_stack.go: an unbounded list of value
+// memories (MaxEntries is not enforced). Elements stay alive after Pop (registers may hold them).
+struct ListMap : Map {
+  bool stack = false;
+  std::vector<ByteMemory*> list;
+  std::vector<std::unique_ptr<ByteMemory>> pool;
+  ByteMemory* make(std::vector<uint8_t>&& b) {
+    auto m = std::make_unique<ByteMemory>();
+    m->region = XE_REGION_QUEUEVAL; m->mapidx = index;
+    m->setBacking(std::move(b));
+    pool.push_back(std::move(m));
+    return pool.back().get();
+  }
+  int Lookup(VM* vm, RV* key, RV** out) override {  // maps_queue.go:39-58, maps_stack.go:38-58
+    if (!isPointer(key)) return ME_KEY_NO_PTR;
+    RV* kr = nullptr;
+    derefRV(vm, key, 0, 4, &kr);  // error ignored (`if !ok`): nil keyVal.Value() panics
+    if (!kr) throw GoPanic{XE_P_NIL_DEREF};
+    const int64_t i = kr->Value();
+    if (i < 0 || i >= int64_t(list.size())) return ME_OOM;
+    *out = vm->mk<MemPtr>(stack ? list[list.size() - 1 - size_t(i)] : list[size_t(i)], 0);
+    return 0;
+  }
+  int Push(VM*, RV* value, int64_t size) override {  // :60-77
+    if (!isPointer(value)) return ME_VAL_NO_PTR;
+    std::vector<uint8_t> vb;
+    if (readRangeRV(value, 0, size, &vb) != 0) vb.clear();
+    list.push_back(make(std::move(vb)));
+    return 0;
+  }
+  int Pop(VM* vm, RV** out) override {  // maps_queue.go:79-91, maps_stack.go:79-90
+    if (list.empty()) { *out = vm->newIMM(0); return 0; }
+    ByteMemory* v = stack ? list.back() : list.front();
+    if (stack) list.pop_back(); else list.erase(list.begin());
+    *out = vm->mk<MemPtr>(v, 0);
+    return 0;
+  }
+};
+
+// PerfEventArray, emulator/maps_perf_event_array.go: an unbounded list of events; Lookup shares the
+// event's bytes (:61-64), Update is not implemented (:67-77).
+struct PerfMap : Map {
+  std::vector<ByteMemory*> events;
+  std::vector<std::unique_ptr<ByteMemory>> pool;
+  int Lookup(VM* vm, RV* key, RV** out) override {  // :45-65
+    if (!isPointer(key)) return ME_KEY_NO_PTR;
+    RV* kr = nullptr;
+    derefRV(vm, key, 0, 4, &kr);
+    if (!kr) throw GoPanic{XE_P_NIL_DEREF};
+    const int64_t kv = kr->Value();
+    if (int64_t(int(kv)) >= int64_t(events.size())) { *out = vm->newIMM(0); return 0; }
+    if (int(kv) < 0) throw GoPanic{XE_P_INDEX};
+    *out = vm->mk<MemPtr>(events[size_t(int(kv))], 0);
+    return 0;
+  }
+  int Update(VM*, RV*, RV*, RV**) override { return ME_NOT_IMPL; }
+  int Push(VM*, RV* value, int64_t size) override {  // :101-115
+    if (!isPointer(value)) return ME_KEY_NO_PTR;
+    std::vector<uint8_t> vb;
+    if (readRangeRV(value, 0, size, &vb) != 0) vb.clear();
+    auto m = std::make_unique<ByteMemory>();
+    m->region = XE_REGION_PERF; m->mapidx = index;
+    m->setBacking(std::move(vb));
+    pool.push_back(std::move(m));
+    events.push_back(pool.back().get());
+    return 0;
+  }
+};
+
 // ---------------------------------------------------------------- registers (registers.go:62-149)
 static int regGet(VM* vm, int r, RV** out) {
   if (r < 0 || r > 9) return XE_E_BAD_REG;
@@ -605,7 +751,7 @@ static int helperErrno(int e) {  // helper_functions.go:57-67
 
 // regToMap, helper_functions.go:109-130. Returns VM error code or 0; *m may be null (R0 = 0 set).
 static int regToMap(VM* vm, RV* reg, Map** m) {
-  int64_t idx = reg->Value();
+  int64_t idx = V(reg);
   if (reg->kind() == XE_KIND_MEMPTR) {
     RV* v = nullptr;
     if (int e = derefRV(vm, reg, 0, 4, &v)) return e;
@@ -620,24 +766,120 @@ static int regToMap(VM* vm, RV* reg, Map** m) {
   return 0;
 }
 
+// errno IMM for a map sentinel error, or the VM error (IN_HELPER-tagged) for any other
+static int mapErr(VM* vm, int me, RV** r0) {
+  if (me & 0x100) return (me & 0xff) | XE_E_IN_HELPER;
+  *r0 = vm->newIMM(helperErrno(me));
+  return 0;
+}
+
+// TailCall, helper_functions.go:133-210
+static int tailCall(VM* vm) {
+  const int64_t mapIdx = V(vm->R[2]);
+  if (mapIdx < 1 || mapIdx >= int64_t(vm->maps.size())) { vm->R[0] = vm->newIMM(-14); return 0; }
+  Map* m = vm->maps[size_t(mapIdx)];
+  if (m->def.type != XE_MAP_PROG_ARRAY) { vm->R[0] = vm->newIMM(-14); return 0; }
+  ValueMemory kmem;  // key: a ValueMemory of 4 slots all holding the R3 object itself
+  kmem.mapping.assign(4, vm->R[3]);
+  MemPtr key(&kmem, 0);
+  RV* valReg = nullptr;
+  if (int me = m->Lookup(vm, &key, &valReg)) {
+    RV* r0 = nullptr;
+    if (int e = mapErr(vm, me, &r0)) return e;
+    vm->R[0] = r0;
+    return 0;
+  }
+  if (!isPointer(valReg)) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "lookup didn't return a pointer"
+  RV* pv = nullptr;
+  if (int e = derefRV(vm, valReg, 0, 4, &pv)) return e | XE_E_IN_HELPER;  // "deref value pointer"
+  const int64_t progIdx = pv->Value();
+  if (int64_t(vm->programs.size()) < progIdx) { vm->R[0] = vm->newIMM(-14); return 0; }  // off by one, :189
+  if (progIdx == 0) return XE_E_NO_PROGRAM | XE_E_IN_HELPER;
+  vm->PI = int(progIdx);
+  vm->PC = -1;
+  vm->R[0] = vm->newIMM(0);
+  return 0;
+}
+
 static int callHelper(VM* vm, int64_t id) {  // returns 0 or VM error code (already IN_HELPER-tagged)
   switch (id) {
     case 1: case 2: {  // MapLookupElement :46-73 / MapUpdateElement :76-101
       Map* m = nullptr;
       if (int e = regToMap(vm, vm->R[1], &m)) return e | XE_E_IN_HELPER;
       if (!m) return 0;
+      if (id == 2) V(vm->R[4]);  // BPFAttrMapElemFlags(R4.Value()) is evaluated first
       RV* val = nullptr;
       int me = id == 1 ? m->Lookup(vm, vm->R[2], &val) : m->Update(vm, vm->R[2], vm->R[3], &val);
-      if (me) {
-        if (me & 0x100) return (me & 0xff) | XE_E_IN_HELPER;
-        val = vm->newIMM(helperErrno(me));
-      }
+      if (me && (me = mapErr(vm, me, &val))) return me;
       vm->R[0] = val;
       return 0;
     }
     case 3: return XE_E_NOT_IMPL | XE_E_IN_HELPER;  // MapDeleteElement :104-106
+    case 12: return tailCall(vm);
     case 14: vm->R[0] = vm->newIMM((int64_t(1234) << 32) + 5678); return 0;  // :213-216
-    case 12: case 25: case 87: case 88: case 89: throw Unsupported{};  // tail call, perf, queue/stack
+    case 25: {  // PerfEventOutput :219-252: R2 = map index (no deref), R4 = data, R5 = size
+      const int64_t mapIdx = V(vm->R[2]);
+      if (mapIdx < 1 || mapIdx >= int64_t(vm->maps.size())) { vm->R[0] = vm->newIMM(-14); return 0; }
+      auto* pa = dynamic_cast<PerfMap*>(vm->maps[size_t(mapIdx)]);
+      if (!pa) { vm->R[0] = vm->newIMM(-14); return 0; }
+      RV* val = vm->newIMM(0);
+      if (int me = pa->Push(vm, vm->R[4], V(vm->R[5])))
+        if ((me = mapErr(vm, me, &val))) return me;
+      vm->R[0] = val;
+      return 0;
+    }
+    case 87: {  // MapPushElement :255-281 (size = ValueSize)
+      Map* m = nullptr;
+      if (int e = regToMap(vm, vm->R[1], &m)) return e | XE_E_IN_HELPER;
+      if (!m) return 0;
+      RV* val = vm->newIMM(0);
+      if (int me = m->Push(vm, vm->R[2], int64_t(m->def.value_size)))
+        if ((me = mapErr(vm, me, &val))) return me;
+      vm->R[0] = val;
+      return 0;
+    }
+    case 88: {  // MapPopElement :284-332
+      Map* m = nullptr;
+      if (int e = regToMap(vm, vm->R[1], &m)) return e | XE_E_IN_HELPER;
+      if (!m) return 0;
+      vm->R[0] = vm->newIMM(0);
+      RV* val = nullptr;
+      if (int me = m->Pop(vm, &val)) {
+        RV* r0 = nullptr;
+        if (int e = mapErr(vm, me, &r0)) return e;
+        vm->R[0] = r0;
+        return 0;
+      }
+      RV* r2 = vm->R[2];
+      if (r2 && r2->kind() == XE_KIND_MEMPTR) {
+        auto* p = static_cast<MemPtr*>(r2);
+        if (int e = p->mem->Write(p->off, val, 8)) return e | XE_E_IN_HELPER;  // "write memory"
+      } else if (r2 && r2->kind() == XE_KIND_FRAMEPTR) {
+        auto* p = static_cast<FramePtr*>(r2);
+        if (int e = p->mem->Write(wadd(p->mem->Size(), p->off), val, 8)) return e | XE_E_IN_HELPER;
+      } else {
+        vm->R[0] = vm->newIMM(-14);
+      }
+      return 0;
+    }
+    case 89: {  // MapPeekElement :335-374: R2 := Lookup(key 0) — nil when the lookup failed
+      Map* m = nullptr;
+      if (int e = regToMap(vm, vm->R[1], &m)) return e | XE_E_IN_HELPER;
+      if (!m) return 0;
+      IMM* k = vm->newIMM(0);
+      ValueMemory kmem;
+      kmem.mapping.assign(4, k);
+      MemPtr key(&kmem, 0);
+      RV* val = nullptr;
+      RV* ret = vm->newIMM(0);
+      if (int me = m->Lookup(vm, &key, &val)) {
+        if ((me = mapErr(vm, me, &ret))) return me;
+        val = nullptr;
+      }
+      vm->R[0] = ret;
+      vm->R[2] = val;
+      return 0;
+    }
   }
   return -1;  // nil helper
 }
@@ -715,7 +957,7 @@ static bool jmpCond(uint8_t op, bool wide, int64_t d, int64_t s) {  // condition
 
 // resolve a pointer register for LDX/ST/STX/atomic: inst_load.go:89-106, inst_store.go:28-43
 static bool ptrTarget(RV* r, int16_t ioff, Memory** mem, int64_t* off) {
-  if (r->kind() == XE_KIND_MEMPTR) {
+  if (KindOf(r) == XE_KIND_MEMPTR) {
     auto* p = static_cast<MemPtr*>(r);
     *off = wadd(p->off, ioff); *mem = p->mem; return true;
   }
@@ -742,12 +984,12 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
       }
       RV* dr = nullptr;
       if (int e = regGet(vm, in.dst, &dr)) return e;
-      int64_t dv = dr->Value();
+      int64_t dv = V(dr);
       int64_t sv = in.imm;
       if (in.reg) {
         RV* sr = nullptr;
         if (int e = regGet(vm, in.src, &sr)) return e;
-        sv = sr->Value();
+        sv = V(sr);
         if (in.op == OP_ADD && isPointer(sr)) {  // inst_add.go:82-98,131-147 pointer edge case
           RV* scp = nullptr;
           regCopy(vm, in.src, &scp);
@@ -765,14 +1007,14 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
     case K_NEG: {  // inst_neg.go:26,51
       RV* dr = nullptr;
       if (int e = regGet(vm, in.dst, &dr)) return e;
-      int64_t dv = dr->Value();
+      int64_t dv = V(dr);
       int64_t v = in.wide ? int64_t(0ull - uint64_t(dv)) : int64_t(int32_t(0u - uint32_t(i32(dv))));
       return assignRV(dr, v);
     }
     case K_END: {  // inst_end.go: to_le swaps, to_be truncates (inverted vs Linux)
       RV* dr = nullptr;
       if (int e = regGet(vm, in.dst, &dr)) return e;
-      uint64_t rv = uint64_t(dr->Value());
+      uint64_t rv = uint64_t(V(dr));
       uint64_t v;
       if (in.op == 0) {
         if (in.imm == 16) v = __builtin_bswap16(uint16_t(rv));
@@ -789,7 +1031,7 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
     case K_JMP: {
       RV* dr = nullptr;
       if (int e = regGet(vm, in.dst, &dr)) return e;
-      int64_t dv = dr->Value();
+      int64_t dv = V(dr);
       bool taken;
       if (!in.reg) {
         bool imm = dr->kind() == XE_KIND_IMM;  // isIMM, inst.go:249-252
@@ -798,8 +1040,9 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
       } else {
         RV* sr = nullptr;
         if (int e = regGet(vm, in.src, &sr)) return e;
+        int64_t sv = V(sr);
         bool same = dr->kind() == sr->kind();  // sameRVType, inst.go:254-258
-        bool c = jmpCond(in.op, in.wide, dv, sr->Value());
+        bool c = jmpCond(in.op, in.wide, dv, sv);
         taken = in.op == J_JNE ? (!same || c) : (same && c);  // inst_jne.go:77,106
       }
       if (taken) vm->PC += in.off;
@@ -861,7 +1104,7 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
       if (int e = mem->Read(off, sz, &dv, vm)) return e;
       RV* sr = nullptr;
       if (int e = regGet(vm, in.src, &sr)) return e;
-      if (int e = assignRV(dv, wadd(dv->Value(), sr->Value()))) return e;
+      if (int e = assignRV(dv, wadd(V(dv), V(sr)))) return e;
       return mem->Write(off, dv, sz);
     }
     case K_CALL: {  // inst_call_helper.go:20-36
@@ -874,7 +1117,7 @@ static int execute(VM* vm, const Inst& in, bool* exit) {
     case K_CALLX: {  // inst_call_helper.go:49-71; Register(imm) truncates to uint8
       RV* fr = nullptr;
       if (int e = regGet(vm, uint8_t(in.imm), &fr)) return e;
-      int64_t fn = fr->Value();
+      int64_t fn = V(fr);
       if (fn >= 192) return XE_E_NO_HELPER;
       if (fn < 0) throw GoPanic{XE_P_INDEX};
       int e = callHelper(vm, fn);
@@ -921,7 +1164,7 @@ static void reset(VM* vm) {
 }
 
 static void regionOf(RV* r, uint8_t* region, uint8_t* map) {
-  if (r->kind() == XE_KIND_IMM) { *region = 0xff; *map = 0; return; }
+  if (!r || r->kind() == XE_KIND_IMM) { *region = 0xff; *map = 0; return; }
   Memory* m = r->kind() == XE_KIND_MEMPTR ? static_cast<MemPtr*>(r)->mem : static_cast<FramePtr*>(r)->mem;
   *region = uint8_t(m->region); *map = uint8_t(m->mapidx);
 }
@@ -970,6 +1213,7 @@ int orc_add_raw_program(orc_vm* o, const uint64_t* insns, uint32_t n, int32_t* i
 int orc_set_entrypoint(orc_vm* o, int32_t idx) {  // vm.go:100-108
   if (idx < 1 || int(o->vm.programs.size()) <= idx) { o->vm.lastError = "program index out of bounds"; return XE_ERR_INVAL; }
   o->vm.PI = idx;
+  o->vm.entry = idx;
   return XE_OK;
 }
 
@@ -989,6 +1233,16 @@ int orc_add_map(orc_vm* o, const xe_map_def* def, const void* init, size_t init_
       m = a;
       break;
     }
+    case XE_MAP_LRU_HASH: case XE_MAP_LRU_PERCPU_HASH:
+      m = new LRUHashMap(); break;
+    case XE_MAP_QUEUE: case XE_MAP_STACK: {
+      auto* l = new ListMap();
+      l->stack = def->type == XE_MAP_STACK;
+      m = l;
+      break;
+    }
+    case XE_MAP_PERF_EVENT_ARRAY:
+      m = new PerfMap(); break;
     default:
       o->vm.lastError = "map type not implemented";
       return XE_ERR_MAPTYPE;
@@ -1005,31 +1259,46 @@ static Map* getMap(orc_vm* o, int32_t i) {
   return o->vm.maps[i];
 }
 
+static std::vector<uint8_t> keyvec(const Map* m, const void* key) {
+  return std::vector<uint8_t>((const uint8_t*)key, (const uint8_t*)key + m->def.key_size);
+}
+static void copyOut(void* dst, const ByteMemory* b, size_t n) {  // value bytes, zero-filled past the backing
+  memset(dst, 0, n);
+  memcpy(dst, b->own.data(), std::min<size_t>(size_t(b->len), n));
+}
+
+// Userspace Map.Lookup: LRU lookups promote the key (maps_hash_lru.go:70-91)
 int orc_map_lookup(orc_vm* o, int32_t mi, const void* key, void* value) {
   Map* m = getMap(o, mi);
   if (!m) return XE_ERR_INVAL;
-  if (m->isHash()) {
-    auto* h = static_cast<HashMap*>(m);
-    std::vector<uint8_t> k((const uint8_t*)key, (const uint8_t*)key + m->def.key_size);
-    auto it = h->values.find(k);
+  if (auto* h = dynamic_cast<HashMap*>(m)) {
+    auto it = h->values.find(keyvec(m, key));
     if (it == h->values.end()) return 0;
-    memset(value, 0, m->def.value_size);
-    memcpy(value, it->second->data(), std::min<int64_t>(it->second->len, m->def.value_size));
+    copyOut(value, it->second.get(), m->def.value_size);
     return 1;
   }
-  auto* a = static_cast<ArrayMap*>(m);
+  if (auto* l = dynamic_cast<LRUHashMap*>(m)) {
+    auto k = keyvec(m, key);
+    auto it = l->values.find(k);
+    if (it == l->values.end()) return 0;
+    l->promote(k);
+    copyOut(value, it->second.get(), m->def.value_size);
+    return 1;
+  }
+  auto* a = dynamic_cast<ArrayMap*>(m);
+  if (!a) return XE_ERR_INVAL;
   uint32_t kv; memcpy(&kv, key, 4);
   if (kv >= m->def.max_entries) return 0;
   memcpy(value, a->memory.own.data() + size_t(kv) * m->def.value_size, m->def.value_size);
   return 1;
 }
 
+// Userspace Map.Update with key/value bytes (flags ignored, as every emulator map does)
 int orc_map_update(orc_vm* o, int32_t mi, const void* key, const void* value) {
   Map* m = getMap(o, mi);
   if (!m) return XE_ERR_INVAL;
-  if (m->isHash()) {
-    auto* h = static_cast<HashMap*>(m);
-    std::vector<uint8_t> k((const uint8_t*)key, (const uint8_t*)key + m->def.key_size);
+  if (auto* h = dynamic_cast<HashMap*>(m)) {
+    auto k = keyvec(m, key);
     auto it = h->values.find(k);
     if (it == h->values.end()) {
       if (h->values.size() + 1 > m->def.max_entries) return XE_ERR_NOMEM;
@@ -1040,7 +1309,25 @@ int orc_map_update(orc_vm* o, int32_t mi, const void* key, const void* value) {
     it->second->setBacking(std::vector<uint8_t>((const uint8_t*)value, (const uint8_t*)value + m->def.value_size));
     return XE_OK;
   }
-  auto* a = static_cast<ArrayMap*>(m);
+  if (auto* l = dynamic_cast<LRUHashMap*>(m)) {  // maps_hash_lru.go:93-161 with byte-backed key/value
+    auto k = keyvec(m, key);
+    auto it = l->values.find(k);
+    if (it == l->values.end()) {
+      if (l->values.size() + 1 > m->def.max_entries) {
+        if (l->usage.empty()) return XE_ERR_NOMEM;
+        l->erase(std::vector<uint8_t>(l->usage.back()));
+      }
+      auto bm = std::make_unique<ByteMemory>();
+      bm->region = XE_REGION_HASHVAL; bm->mapidx = mi;
+      it = l->values.emplace(k, std::move(bm)).first;
+      l->usage.push_back(k);
+    }
+    l->promote(k);
+    it->second->setBacking(std::vector<uint8_t>((const uint8_t*)value, (const uint8_t*)value + m->def.value_size));
+    return XE_OK;
+  }
+  auto* a = dynamic_cast<ArrayMap*>(m);
+  if (!a) return XE_ERR_INVAL;
   uint32_t kv; memcpy(&kv, key, 4);
   if (kv >= m->def.max_entries) return XE_ERR_INVAL;
   memcpy(a->memory.own.data() + size_t(kv) * m->def.value_size, value, m->def.value_size);
@@ -1050,7 +1337,7 @@ int orc_map_update(orc_vm* o, int32_t mi, const void* key, const void* value) {
 int orc_map_update_batch(orc_vm* o, int32_t mi, const void* keys, const void* values, uint64_t count) {
   Map* m = getMap(o, mi);
   if (!m) return XE_ERR_INVAL;
-  const size_t ks = m->isHash() ? m->def.key_size : 4, vs = m->def.value_size;
+  const size_t ks = dynamic_cast<ArrayMap*>(m) ? 4 : m->def.key_size, vs = m->def.value_size;
   for (uint64_t i = 0; i < count; i++)
     if (int rc = orc_map_update(o, mi, (const uint8_t*)keys + i * ks, (const uint8_t*)values + i * vs)) return rc;
   return XE_OK;
@@ -1058,48 +1345,102 @@ int orc_map_update_batch(orc_vm* o, int32_t mi, const void* keys, const void* va
 
 int orc_map_delete(orc_vm* o, int32_t mi, const void* key) {
   Map* m = getMap(o, mi);
-  if (!m || !m->isHash()) return XE_ERR_INVAL;
-  auto* h = static_cast<HashMap*>(m);
-  std::vector<uint8_t> k((const uint8_t*)key, (const uint8_t*)key + m->def.key_size);
-  h->values.erase(k);
+  if (!m) return XE_ERR_INVAL;
+  if (auto* h = dynamic_cast<HashMap*>(m)) { h->values.erase(keyvec(m, key)); return XE_OK; }
+  if (auto* l = dynamic_cast<LRUHashMap*>(m)) { l->erase(keyvec(m, key)); return XE_OK; }
+  return XE_ERR_INVAL;
+}
+
+// QueueMap/StackMap.Push from userspace: one value_size element
+int orc_map_push(orc_vm* o, int32_t mi, const void* value) {
+  Map* m = getMap(o, mi);
+  auto* l = dynamic_cast<ListMap*>(m);
+  if (!l) return XE_ERR_INVAL;
+  l->list.push_back(l->make(std::vector<uint8_t>((const uint8_t*)value, (const uint8_t*)value + m->def.value_size)));
   return XE_OK;
 }
 
 int orc_map_count(orc_vm* o, int32_t mi, uint64_t* count) {
   Map* m = getMap(o, mi);
   if (!m) return XE_ERR_INVAL;
-  *count = m->isHash() ? static_cast<HashMap*>(m)->values.size() : m->def.max_entries;
+  if (auto* h = dynamic_cast<HashMap*>(m)) *count = h->values.size();
+  else if (auto* l = dynamic_cast<LRUHashMap*>(m)) *count = l->values.size();
+  else if (auto* q = dynamic_cast<ListMap*>(m)) *count = q->list.size();
+  else if (auto* p = dynamic_cast<PerfMap*>(m)) *count = p->events.size();
+  else *count = m->def.max_entries;
   return XE_OK;
 }
 
-// MA6: ARRAY = raw bytes; HASH = (key, value) sorted by key bytes. A nil-backed value (HashMap
-// Update whose value ReadRange failed, maps_hash.go:108-115) dumps as zeros; its key as stored.
+// MA6: ARRAY = raw bytes; HASH / LRU_HASH = (key, value) sorted by key bytes. A nil-backed value
+// (Update whose value ReadRange failed, maps_hash.go:108-115) dumps as zeros; its key as stored.
 int orc_map_dump(orc_vm* o, int32_t mi, void* keys_or_raw, void* values, uint64_t cap, uint64_t* count) {
   Map* m = getMap(o, mi);
   if (!m) return XE_ERR_INVAL;
-  if (!m->isHash()) {
-    auto* a = static_cast<ArrayMap*>(m);
+  if (auto* a = dynamic_cast<ArrayMap*>(m)) {
     if (count) *count = m->def.max_entries;
     if (keys_or_raw && cap >= m->def.max_entries) memcpy(keys_or_raw, a->memory.own.data(), a->memory.own.size());
     return XE_OK;
   }
-  auto* h = static_cast<HashMap*>(m);
-  if (count) *count = h->values.size();
+  const std::map<std::vector<uint8_t>, std::unique_ptr<ByteMemory>>* vals = nullptr;
+  if (auto* h = dynamic_cast<HashMap*>(m)) vals = &h->values;
+  else if (auto* l = dynamic_cast<LRUHashMap*>(m)) vals = &l->values;
+  if (!vals) {  // list maps: values in list order (use orc_map_dump_list for the lengths)
+    uint64_t n = 0;
+    orc_map_count(o, mi, &n);
+    if (count) *count = n;
+    return XE_OK;
+  }
+  if (count) *count = vals->size();
   if (!keys_or_raw && !values) return XE_OK;
-  if (cap < h->values.size()) return XE_ERR_INVAL;
+  if (cap < vals->size()) return XE_ERR_INVAL;
   size_t i = 0;
-  for (auto& kv : h->values) {  // std::map iterates in lexicographic key order
+  for (auto& kv : *vals) {  // std::map iterates in lexicographic key order
     if (keys_or_raw) {
       uint8_t* kd = (uint8_t*)keys_or_raw + i * m->def.key_size;
       memset(kd, 0, m->def.key_size);
       memcpy(kd, kv.first.data(), std::min<size_t>(kv.first.size(), m->def.key_size));
     }
-    if (values) {
-      uint8_t* vd = (uint8_t*)values + i * m->def.value_size;
-      memset(vd, 0, m->def.value_size);
-      memcpy(vd, kv.second->data(), std::min<int64_t>(kv.second->len, m->def.value_size));
-    }
+    if (values) copyOut((uint8_t*)values + i * m->def.value_size, kv.second.get(), m->def.value_size);
     i++;
+  }
+  return XE_OK;
+}
+
+// QUEUE / STACK / PERF_EVENT_ARRAY: records in list order (Values / Events slice order)
+int orc_map_dump_list(orc_vm* o, int32_t mi, void* data, uint64_t data_cap, uint32_t* lens, uint64_t cap,
+                      uint64_t* count, uint64_t* bytes) {
+  Map* m = getMap(o, mi);
+  const std::vector<ByteMemory*>* list = nullptr;
+  if (auto* q = dynamic_cast<ListMap*>(m)) list = &q->list;
+  else if (auto* p = dynamic_cast<PerfMap*>(m)) list = &p->events;
+  if (!list) return XE_ERR_INVAL;
+  uint64_t total = 0;
+  for (auto* b : *list) total += uint64_t(b->len);
+  if (count) *count = list->size();
+  if (bytes) *bytes = total;
+  if (!data && !lens) return XE_OK;
+  if (cap < list->size() || (data && data_cap < total)) return XE_ERR_INVAL;
+  uint64_t off = 0;
+  for (size_t i = 0; i < list->size(); i++) {
+    const ByteMemory* b = (*list)[i];
+    if (lens) lens[i] = uint32_t(b->len);
+    if (data && b->len) memcpy((uint8_t*)data + off, b->own.data(), size_t(b->len));
+    off += uint64_t(b->len);
+  }
+  return XE_OK;
+}
+
+// LRU_HASH UsageList, most recently used first
+int orc_map_lru_order(orc_vm* o, int32_t mi, void* keys, uint64_t cap, uint64_t* count) {
+  auto* l = dynamic_cast<LRUHashMap*>(getMap(o, mi));
+  if (!l) return XE_ERR_INVAL;
+  if (count) *count = l->usage.size();
+  if (!keys) return XE_OK;
+  if (cap < l->usage.size()) return XE_ERR_INVAL;
+  for (size_t i = 0; i < l->usage.size(); i++) {
+    uint8_t* kd = (uint8_t*)keys + i * l->def.key_size;
+    memset(kd, 0, l->def.key_size);
+    memcpy(kd, l->usage[i].data(), std::min<size_t>(l->usage[i].size(), l->def.key_size));
   }
   return XE_OK;
 }
@@ -1113,6 +1454,9 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
   if (stats) memset(stats, 0, sizeof *stats);
   for (uint32_t p = 0; p < n; p++) {
     reset(&vm);
+    // Reset keeps PI (emulator/vm.go:211-246); a tail call in the previous packet would otherwise
+    // start this one in another program: the harness re-applies SetEntrypoint per packet
+    vm.PI = vm.entry;
     ByteMemory pkt;
     pkt.region = XE_REGION_PACKET;
     uint64_t a = desc[p].addr, l = desc[p].len;
@@ -1134,7 +1478,10 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
       for (;;) {  // RunContext, vm.go:117-134
         if (vm.steps >= vm.settings.max_steps) { res.status = XE_ST_BUDGET; res.pc = uint32_t(vm.PC); break; }
         // Step, vm.go:137-173
-        if (vm.PI < 1 || vm.PI >= int(vm.programs.size())) { res.status = XE_ST_VMERR; res.code = XE_E_NO_PROGRAM; break; }
+        if (vm.PI < 1 || vm.PI >= int(vm.programs.size())) {
+          res.status = XE_ST_VMERR; res.code = XE_E_NO_PROGRAM; res.pc = uint32_t(vm.PC);
+          break;
+        }
         const auto& prog = vm.programs[vm.PI];
         if (vm.PC < 0 || vm.PC >= int64_t(prog.size())) throw GoPanic{XE_P_INDEX};  // program[PC]
         int64_t pc = vm.PC;
@@ -1156,16 +1503,16 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
     } catch (Unsupported&) {
       res.status = XE_ST_UNSUPPORTED; res.pc = uint32_t(vm.PC);
     }
-    res.r0_kind = uint8_t(vm.R[0]->kind());
-    res.r0 = vm.R[0]->Value();
+    res.r0_kind = uint8_t(vm.R[0] ? vm.R[0]->kind() : XE_KIND_NIL);
+    res.r0 = vm.R[0] ? vm.R[0]->Value() : 0;
     if (results) results[p] = res;
     if (verdicts) verdicts[p] = uint32_t(uint64_t(res.r0));
     if (regs) {
       xe_regs& rg = regs[p];
       memset(&rg, 0, sizeof rg);
       for (int r = 0; r < 10; r++) {
-        rg.val[r] = vm.R[r]->Value();
-        rg.kind[r] = uint8_t(vm.R[r]->kind());
+        rg.val[r] = vm.R[r] ? vm.R[r]->Value() : 0;
+        rg.kind[r] = uint8_t(vm.R[r] ? vm.R[r]->kind() : XE_KIND_NIL);
         regionOf(vm.R[r], &rg.region[r], &rg.map[r]);
       }
       rg.steps = uint32_t(vm.steps);

@@ -26,6 +26,10 @@ int orc_map_delete(orc_vm* vm, int32_t map_idx, const void* key);
 int orc_map_update_batch(orc_vm* vm, int32_t map_idx, const void* keys, const void* values, uint64_t count);
 int orc_map_count(orc_vm* vm, int32_t map_idx, uint64_t* count);
 int orc_map_dump(orc_vm* vm, int32_t map_idx, void* keys_or_raw, void* values, uint64_t cap, uint64_t* count);
+int orc_map_dump_list(orc_vm* vm, int32_t map_idx, void* data, uint64_t data_cap, uint32_t* lens, uint64_t cap,
+                      uint64_t* count, uint64_t* bytes);
+int orc_map_lru_order(orc_vm* vm, int32_t map_idx, void* keys, uint64_t cap, uint64_t* count);
+int orc_map_push(orc_vm* vm, int32_t map_idx, const void* value);
 /* Sequential per-packet harness over host memory; packet writes land in umem. */
 int orc_run_batch(orc_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* desc, uint32_t n,
                   xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);

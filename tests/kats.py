@@ -7,9 +7,11 @@ from __future__ import annotations
 
 from gobpfld_amd.asm import (ADD, ARSH, DIV, JEQ, JGT, JNE, JSGE, JSGT, JSLE, JSLT, LSH, MOD, MUL,
                              RSH, SUB, XOR, Asm, AND, OR)
-from gobpfld_amd.emulator import MAP_ARRAY, MAP_HASH, MapDef
+from gobpfld_amd.emulator import (MAP_ARRAY, MAP_HASH, MAP_LRU_HASH, MAP_PERF_EVENT_ARRAY, MAP_PROG_ARRAY, MAP_QUEUE,
+                                  MAP_STACK, MapDef)
 
 OK, VMERR, PANIC, BUDGET, UNSUP = 0, 1, 2, 3, 4
+E_NO_PROGRAM = 1
 E_BAD_REG, E_ASSIGN_REG, E_READONLY, E_DIV0, E_NONPTR_LOAD, E_NONPTR_STORE = 2, 3, 4, 5, 6, 7
 E_OOB, E_NONCONTIG, E_UNINIT, E_BAD_PC, E_NOT_IMPL, E_NO_HELPER, E_NO_MAP, E_MAP_NOT_PTR = 8, 9, 10, 11, 12, 13, 14, 15
 IN_HELPER = 0x80
@@ -30,11 +32,17 @@ def _s64(v):
 KATS: list[dict] = []
 
 
-def kat(name, expect=None, maps=(), entries=None, pkt=64, cite=""):
+def kat(name, expect=None, maps=(), entries=None, pkt=64, cite="", extra=()):
+    """extra: more programs (Asm builders) added after the entrypoint, as VM programs 2, 3, ..."""
     def deco(fn):
         a = Asm()
         fn(a)
-        KATS.append(dict(name=name, program=a.assemble(), maps=list(maps), entries=entries or {},
+        progs = [a.assemble()]
+        for f in extra:
+            b = Asm()
+            f(b)
+            progs.append(b.assemble())
+        KATS.append(dict(name=name, program=progs if extra else progs[0], maps=list(maps), entries=entries or {},
                          expect=expect, pkt=pkt, cite=cite))
         return fn
     return deco
@@ -486,9 +494,9 @@ def _(a):
     a.label("out").mov64(0, 0).exit()
 
 
-@kat("tail_call_unsupported", (UNSUP, None), maps=[ARRAY8], cite="helper_functions.go:133-210 (out of scope)")
+@kat("tail_call_bad_map_index_efault", (OK, -14), maps=[ARRAY8], cite="helper_functions.go:135-139 (R2 = IMM 0 after Reset)")
 def _(a):
-    a.call(12).mov64(0, 0).exit()
+    a.call(12).exit()
 
 
 @kat("ld_abs_not_implemented", (VMERR, E_NOT_IMPL), cite="emulator/inst_load.go:146-148")
@@ -499,3 +507,273 @@ def _(a):
 @kat("callx_dispatch", (OK, (1234 << 32) + 5678), cite="emulator/inst_call_helper.go:49-71")
 def _(a):
     a.mov64(3, 14).emit(0x8D, 0, 0, 0, 3).exit()
+
+
+# ---- ValueMemory objects beyond the fields model's 57 (emulator/memory.go:97-107: every stored byte
+# may hold its own object; the device's general model keeps them in its arena)
+@kat("capacity_64_byte_stores", (OK, 63), cite="emulator/memory.go:97-107 (64 live objects on the stack)")
+def _(a):
+    for i in range(64):
+        a.st(1, 10, -(i + 1), i)
+    a.ldx(1, 0, 10, -64).exit()
+
+
+@kat("capacity_ctx_and_stack", (OK, 23 * 256 + 39), cite="emulator/memory.go:97-107 (24 ctx + 40 stack objects)")
+def _(a):
+    for i in range(24):
+        a.st(1, 1, i, i)
+    for i in range(40):
+        a.st(1, 10, -(i + 1), i)
+    a.ldx(1, 2, 1, 23).ldx(1, 3, 10, -40).mov64(0, src=2).alu64(MUL, 0, 256).add64(0, src=3).exit()
+
+
+@kat("capacity_loop_256_objects", (OK, 7 * 256 + 255), cite="emulator/memory.go:97-107 (a loop fills the frame)")
+def _(a):
+    a.mov64(2, 0)
+    a.label("loop").mov64(3, src=10).add64(3, -256).add64(3, src=2).stx(1, 3, 0, 2)
+    a.add64(2, 1).jmp(JNE, 2, "loop", imm=256)
+    a.ldx(1, 0, 10, -256).alu64(MUL, 0, 256).ldx(1, 4, 10, -1).add64(0, src=4)
+    a.mov64(5, 7).alu64(MUL, 5, 256).add64(0, src=5).exit()
+
+
+# ---- bpf-to-bpf calls (emulator/inst_call_bpf.go:18-44, emulator/inst_exit.go:22-48)
+@kat("callbpf_basic", (OK, 11), cite="inst_call_bpf.go:41 (PC += imm), inst_exit.go:33-37")
+def _(a):
+    a.mov64(1, 5).call_bpf("sub").add64(0, 1).exit()
+    a.label("sub").mov64(0, src=1).alu64(MUL, 0, 2).exit()
+
+
+@kat("callbpf_own_stack_frame", (OK, 111), cite="inst_call_bpf.go:23-39 (R10 := next frame, wiped)")
+def _(a):
+    a.st(8, 10, -8, 111).call_bpf("sub").ldx(8, 0, 10, -8).exit()
+    a.label("sub").st(8, 10, -8, 222).mov64(0, 0).exit()
+
+
+@kat("callbpf_r6_clone_sees_old_stack", (OK, 5 * 16 + 9), cite="registers.go:44-60,294-303 (R6-R9 deep clones)")
+def _(a):
+    a.st(8, 10, -8, 5).mov64(6, src=10).add64(6, -8).mov64(1, src=10).add64(1, -8)
+    a.call_bpf("sub")
+    a.ldx(8, 2, 6, 0).ldx(8, 3, 10, -8).mov64(0, src=2).alu64(MUL, 0, 16).add64(0, src=3).exit()
+    a.label("sub").st(8, 1, 0, 9).mov64(0, 0).exit()
+
+
+@kat("callbpf_r7_clone_of_packet", (OK, None), cite="registers.go:233-240 + memory.go:212-219 (packet bytes copied)")
+def _(a):
+    a.mov64(8, src=1).ldx(4, 7, 1, 0).mov64(1, src=7).call_bpf("sub")
+    a.ldx(1, 2, 7, 0).ldx(4, 3, 8, 0).ldx(1, 3, 3, 0).mov64(0, src=2).alu64(MUL, 0, 256).add64(0, src=3).exit()
+    a.label("sub").mov64(6, src=1).st(1, 1, 0, 0xAB).mov64(0, 0).exit()
+
+
+@kat("callbpf_r6_clone_of_map_value", (OK, None), maps=[ARRAY8], cite="registers.go:233-240 (the array memory is copied)")
+def _(a):
+    a.st(4, 10, -4, 1).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "out", imm=0)
+    a.mov64(6, src=0).mov64(1, src=0).call_bpf("sub")
+    a.ldx(8, 2, 6, 0).mov64(0, src=2).exit()
+    a.label("out").mov64(0, -1).exit()
+    a.label("sub").mov64(2, 5).stx(8, 1, 0, 2).mov64(0, 0).exit()
+
+
+@kat("callbpf_frame_overflow_panics", (PANIC, P_INDEX), cite="inst_call_bpf.go:23-28 (&StackFrames[8])")
+def _(a):
+    a.call_bpf("sub").exit()
+    a.label("sub").call_bpf("sub").exit()
+
+
+@kat("callbpf_depth_7_ok", (OK, 7), cite="inst_call_bpf.go:23-28 (frames 1..7 exist)")
+def _(a):
+    a.mov64(0, 0).call_bpf("f1").exit()
+    for k in range(1, 8):
+        a.label(f"f{k}").add64(0, 1)
+        if k < 7:
+            a.call_bpf(f"f{k + 1}")
+        a.exit()
+
+
+# ---- tail calls (emulator/helper_functions.go:133-210)
+PROGS = (MapDef(MAP_PROG_ARRAY, 4, 4, 4), None)
+
+
+def _prog_table(*idx):
+    """PROG_ARRAY contents as host-side updates (AbstractMapToVM gives PROG_ARRAY no InitialData)."""
+    return {0: [(int(k).to_bytes(4, "little"), int(i).to_bytes(4, "little")) for k, i in enumerate(idx)]}
+
+
+def _tail(a, key=0, after=99):
+    a.ld_map(2, 1).mov64(3, key).call(12).mov64(0, after).exit()
+
+
+@kat("tail_call_runs_target", (OK, 42), maps=[PROGS], entries=_prog_table(2),
+     cite="helper_functions.go:198-208", extra=[lambda b: b.mov64(0, 42).exit()])
+def _(a):
+    _tail(a)
+
+
+@kat("tail_call_keeps_registers_and_stack", (OK, 7 + 100), maps=[PROGS], entries=_prog_table(2),
+     cite="helper_functions.go:203-205 (no Reset)",
+     extra=[lambda b: b.ldx(8, 0, 10, -8).add64(0, src=6).exit()])
+def _(a):
+    a.st(8, 10, -8, 7).mov64(6, 100)
+    _tail(a)
+
+
+@kat("tail_call_off_by_one_no_program", (VMERR, E_NO_PROGRAM), maps=[PROGS], entries=_prog_table(3),
+     cite="helper_functions.go:189 (len(Programs) < idx lets idx == len through)", extra=[lambda b: b.mov64(0, 1).exit()])
+def _(a):
+    _tail(a)
+
+
+@kat("tail_call_index_too_large_efault", (OK, -14), maps=[PROGS], entries=_prog_table(4),
+     cite="helper_functions.go:189-192", extra=[lambda b: b.mov64(0, 1).exit()])
+def _(a):
+    a.ld_map(2, 1).mov64(3, 0).call(12).exit()
+
+
+@kat("tail_call_zero_index_vmerr", (VMERR, E_NO_PROGRAM | IN_HELPER), maps=[PROGS], entries=_prog_table(0),
+     cite="helper_functions.go:194-196")
+def _(a):
+    _tail(a)
+
+
+@kat("tail_call_key_beyond_array", (VMERR, 16 | IN_HELPER), maps=[PROGS], entries=_prog_table(2),
+     cite="helper_functions.go:178-181 (Lookup returned IMM 0)", extra=[lambda b: b.mov64(0, 1).exit()])
+def _(a):
+    _tail(a, key=9)
+
+
+@kat("tail_call_not_prog_array_efault", (OK, -14), maps=[ARRAY8], cite="helper_functions.go:143-146")
+def _(a):
+    a.ld_map(2, 1).mov64(3, 0).call(12).exit()
+
+
+# ---- LRU hash (emulator/maps_hash_lru.go)
+LRU2 = (MapDef(MAP_LRU_HASH, 4, 8, 2), None)
+
+
+def _lru_update(a, key, val):
+    a.st(4, 10, -4, key).st(8, 10, -16, val).ld_map(1, 1).mov64(2, src=10).add64(2, -4)
+    a.mov64(3, src=10).add64(3, -16).mov64(4, 0).call(2)
+
+
+def _lru_lookup(a, key):
+    a.st(4, 10, -4, key).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+
+
+@kat("lru_evicts_least_recently_used", (OK, 20), maps=[LRU2], cite="maps_hash_lru.go:114-119")
+def _(a):
+    _lru_update(a, 1, 10)
+    _lru_update(a, 2, 20)
+    _lru_lookup(a, 1)   # 1 becomes most recent: 2 is now the LRU
+    _lru_update(a, 3, 30)  # evicts 2
+    _lru_lookup(a, 2)
+    a.mov64(6, src=0)
+    _lru_lookup(a, 1)
+    a.ldx(8, 0, 0, 0).add64(0, 10)   # r0 = 10 + 10
+    a.exit()
+
+
+@kat("lru_update_non_pointer_value_still_evicts", (OK, -14), maps=[(MapDef(MAP_LRU_HASH, 4, 8, 1), None)],
+     cite="maps_hash_lru.go:114-137 (eviction precedes the value check)")
+def _(a):
+    _lru_update(a, 1, 10)
+    a.st(4, 10, -4, 2).ld_map(1, 1).mov64(2, src=10).add64(2, -4).mov64(3, 0).mov64(4, 0).call(2).exit()
+
+
+# ---- queue / stack (emulator/maps_queue.go, maps_stack.go; helper_functions.go:255-374)
+Q8 = (MapDef(MAP_QUEUE, 0, 8, 16), None)
+S8 = (MapDef(MAP_STACK, 0, 8, 16), None)
+
+
+def _push(a, val):
+    a.st(8, 10, -8, val).ld_map(1, 1).mov64(2, src=10).add64(2, -8).call(87)
+
+
+def _pop_deref(a):
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -24).call(88)
+    a.ldx(8, 3, 10, -24).ldx(8, 0, 3, 0).exit()   # the popped MemoryPtr object, then its bytes
+
+
+@kat("queue_pop_is_fifo", (OK, 5), maps=[Q8], cite="maps_queue.go:79-91, helper_functions.go:311-324")
+def _(a):
+    _push(a, 5)
+    _push(a, 6)
+    _push(a, 7)
+    _pop_deref(a)
+
+
+@kat("stack_pop_is_lifo", (OK, 7), maps=[S8], cite="maps_stack.go:79-90")
+def _(a):
+    _push(a, 5)
+    _push(a, 6)
+    _push(a, 7)
+    _pop_deref(a)
+
+
+@kat("queue_lookup_by_index", (OK, 6), maps=[Q8], cite="maps_queue.go:39-58")
+def _(a):
+    _push(a, 5)
+    _push(a, 6)
+    a.st(4, 10, -4, 1).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1).ldx(8, 0, 0, 0).exit()
+
+
+@kat("queue_lookup_out_of_range_e2big", (OK, -7), maps=[Q8], cite="maps_queue.go:50-52")
+def _(a):
+    a.st(4, 10, -4, 3).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1).exit()
+
+
+@kat("peek_empty_queue_e2big_and_nil_r2", (OK, -7), maps=[Q8], cite="helper_functions.go:356-371 (R2 := nil)")
+def _(a):
+    a.ld_map(1, 1).call(89).exit()
+
+
+@kat("nil_register_use_panics", (PANIC, P_NIL_DEREF), maps=[Q8], cite="helper_functions.go:371 then registers.go Copy")
+def _(a):
+    a.ld_map(1, 1).call(89).mov64(0, src=2).exit()
+
+
+@kat("peek_queue_front", (OK, 5), maps=[Q8], entries={0: [(None, (5).to_bytes(8, "little")), (None, (6).to_bytes(8, "little"))]},
+     cite="helper_functions.go:345-372 (R2 := pointer to Values[0])")
+def _(a):
+    a.ld_map(1, 1).call(89).ldx(8, 0, 2, 0).exit()
+
+
+@kat("push_on_array_map_vmerr", (VMERR, 16 | IN_HELPER), maps=[ARRAY8], cite="maps.go:76-78 (push not available)")
+def _(a):
+    _push(a, 1)
+    a.exit()
+
+
+@kat("pop_empty_writes_imm_zero", (OK, 0), maps=[Q8], cite="maps_queue.go:80-82 + helper_functions.go:311-324")
+def _(a):
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -8).call(88).ldx(8, 0, 10, -8).exit()
+
+
+# ---- perf event output (emulator/helper_functions.go:219-252, maps_perf_event_array.go:101-115)
+PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
+
+
+@kat("perf_output_appends_event", (OK, 0), maps=[PERF], cite="helper_functions.go:219-252")
+def _(a):
+    a.st(8, 10, -8, 0x1234).ld_map(2, 1).mov64(4, src=10).add64(4, -8).mov64(5, 8).call(25).exit()
+
+
+@kat("perf_output_stack_run_widened_panics", (PANIC, P_INDEX), maps=[PERF],
+     cite="memory.go:69-91 (a 6-byte read of an 8-byte object widens to 8: r[i:i+8] past 6)")
+def _(a):
+    a.st(8, 10, -8, 0x1234).ld_map(2, 1).mov64(4, src=10).add64(4, -8).mov64(5, 6).call(25).exit()
+
+
+@kat("perf_output_from_packet", (OK, 0), maps=[PERF], cite="maps_perf_event_array.go:101-115 (ReadRange of R4)")
+def _(a):
+    a.ldx(4, 4, 1, 0).ld_map(2, 1).mov64(5, 20).call(25).exit()
+
+
+@kat("perf_output_negative_size_panics", (PANIC, 6), maps=[PERF], cite="memory.go:181 make([]byte, negative)")
+def _(a):
+    a.ldx(4, 4, 1, 0).ld_map(2, 1).mov64(5, -1).call(25).exit()
+
+
+@kat("perf_lookup_shares_event", (OK, 0x34), maps=[PERF], cite="maps_perf_event_array.go:45-65")
+def _(a):
+    a.st(8, 10, -8, 0x1234).ld_map(2, 1).mov64(4, src=10).add64(4, -8).mov64(5, 8).call(25)
+    a.st(4, 10, -12, 0).ld_map(1, 1).mov64(2, src=10).add64(2, -12).call(1).ldx(1, 0, 0, 0).exit()

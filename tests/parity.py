@@ -20,14 +20,29 @@ def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=N
         idx.append(m)
         if entries and i in entries:
             for k, v in entries[i]:
-                vm.map_update(m, k, v)
-    p = vm.add_raw_program(program)
+                if k is None:
+                    vm.map_push(m, v)  # QUEUE / STACK element
+                else:
+                    vm.map_update(m, k, v)
+    # `program` may be a list of programs: the first is the entrypoint (tail-call targets follow)
+    progs = program if program and isinstance(program[0], list) else [program]
+    p = [vm.add_raw_program(x) for x in progs][0]
     vm.set_entrypoint(p)
     mem = umem.copy()
     r = vm.run_batch(mem, descs, want_regs=regs)
-    dumps = [vm.map_dump(m) for m in idx]
+    dumps = [_dump(vm, m) for m in idx]
     vm.close()
     return r, dumps, mem
+
+
+def _dump(vm, m):
+    """Final state of map m: ARRAY raw bytes, HASH (keys, values), LRU_HASH (keys, values) + UsageList,
+    QUEUE / STACK / PERF list of records."""
+    from gobpfld_amd.emulator import MAP_LRU_HASH, MAP_LRU_PERCPU_HASH
+    d = vm.map_dump(m)
+    if vm.map_defs[m].type in (MAP_LRU_HASH, MAP_LRU_PERCPU_HASH):
+        return {"entries_keys": d[0], "entries_values": d[1], "usage": vm.map_lru_order(m)}
+    return d
 
 
 def assert_same(a, b, what=""):
@@ -46,8 +61,12 @@ def assert_same(a, b, what=""):
     assert (ra.verdicts == rb.verdicts).all(), f"{what}: verdicts differ"
     assert np.array_equal(ma, mb), f"{what}: packet bytes differ"
     for j, (x, y) in enumerate(zip(da, db)):
-        if isinstance(x, bytes):
-            assert x == y, f"{what}: array map {j + 1} differs"
+        if isinstance(x, (bytes, list)):
+            assert x == y, f"{what}: map {j + 1} differs"
+        elif isinstance(x, dict):
+            assert x.keys() == y.keys()
+            for k in x:
+                assert np.array_equal(x[k], y[k]) if isinstance(x[k], np.ndarray) else x[k] == y[k], f"{what}: map {j + 1} {k} differs"
         else:
             assert len(x[0]) == len(y[0]), f"{what}: hash map {j + 1} entry count {len(x[0])} vs {len(y[0])}"
             assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]), f"{what}: hash map {j + 1} differs"

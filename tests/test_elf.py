@@ -123,18 +123,22 @@ def test_elf_programs_oracle_known_answers(oracle_lib):
     assert (r.results["status"] == 0).all() and (r.results["r0"] == 15).all()
 
 
-@pytest.mark.parametrize("which", ["stats", "rodata"])
+def _obj(which):
+    return {"stats": lambda: stats_object()[0], "rodata": rodata_object, "call": call_object}[which]()
+
+
+@pytest.mark.parametrize("which", ["stats", "rodata", "call"])
 def test_elf_programs_hostsim_equal_oracle(oracle_lib, hostsim_lib, which):
-    data = stats_object()[0] if which == "stats" else rodata_object()
+    data = _obj(which)
     obj = E.parse_elf(data)
     prog = next(iter(obj.programs))
     assert_same(_run(hostsim_lib, obj, prog), _run(oracle_lib, obj, prog), f"elf {which}")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("which", ["stats", "rodata"])
+@pytest.mark.parametrize("which", ["stats", "rodata", "call"])
 def test_elf_programs_device_equal_oracle(gpu_lib, oracle_lib, which):
-    data = stats_object()[0] if which == "stats" else rodata_object()
+    data = _obj(which)
     obj = E.parse_elf(data)
     prog = next(iter(obj.programs))
     assert_same(_run(gpu_lib, obj, prog, n=4096), _run(oracle_lib, obj, prog, n=4096), f"elf {which} (device)")

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from gobpfld_amd import workloads as W
-from gobpfld_amd.emulator import ENGINE_INTERP, ENGINE_JIT, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
+from gobpfld_amd.emulator import EmulatorError, ENGINE_INTERP, ENGINE_JIT, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
 from kats import KATS
 from parity import assert_same, config_case, packets, run_one
 
@@ -21,7 +21,12 @@ ENGINE_IDS = ["interp", "jit"]
 @pytest.mark.parametrize("k", KATS, ids=[k["name"] for k in KATS])
 def test_kat_device_equals_oracle(gpu_lib, oracle_lib, k, engine):
     umem, descs = packets(64, k["pkt"], seed=7)
-    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"], settings=Settings(engine=engine))
+    try:
+        a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"], settings=Settings(engine=engine))
+    except EmulatorError as e:
+        # calls, tail calls and ordered maps live in the interpreter's general model only
+        assert engine == ENGINE_JIT and "general model" in str(e), str(e)
+        pytest.skip("interpreter-only program")
     assert a[0].stats["engine_used"] == engine
     b = run_one(oracle_lib, k["program"], k["maps"], umem, descs, entries=k["entries"])
     assert_same(a, b, k["name"])

@@ -31,6 +31,8 @@ WORKLOADS = {
     "c3": "C3: 5-tuple HASH lookup -> REDIRECT + hit counter, 64K flows, IMIX 64/576/1500 B",
     "c4": "C4: ~200-insn JEQ/JGT ACL (48 rules), 1500 B packets, lane-divergence stress",
     "c5": "C5: C2 parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets",
+    "c2rmw": "C2-RMW: C2 with the per-proto counter bumped by a plain load/add/store (value->packets++ without "
+             "an atomic): the ordered read-modify-write, run in parallel through lift_rmw",
 }  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec peak
 
 
@@ -164,6 +166,35 @@ def e2e_baseline(vm, umem: np.ndarray, descs: np.ndarray, iters: int = 3) -> dic
             "path": "pinned host UMEM + descriptors -> H2D -> kernel -> D2H verdicts (xe_run_batch_host)"}
 
 
+def ordered_paths(d_umem, d_desc, n: int, dev, stream, seq_sample: int = 65536) -> dict:
+    """C2-RMW (C2 with `value->packets++` as a plain load/add/store) on the C2 batch: the lifted
+    parallel path over all n packets (lift_rmw), and, for scale, the one-lane ordered replay the
+    same program takes without lifting (MODE_SEQUENTIAL) on the first `seq_sample` packets."""
+    import torch
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import MODE_SEQUENTIAL, VM, Settings
+    d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    out = {"program": WORKLOADS["c2rmw"]}
+    for key, mode, cnt, reps in (("lifted_parallel", 0, n, 5), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
+        vm = VM(Settings(device=dev.index or 0, mode=mode))
+        W.setup_vm(vm, "c2rmw")
+        run = lambda: vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), cnt,
+                                          d_verdicts=d_ver.data_ptr(), stream=stream)
+        run()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ks = []
+        for _ in range(reps):
+            st = run()
+            ks.append(st["kernel_ms"])
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / reps
+        out[key] = {"value": round(cnt / dt / 1e6, 3), "unit": "Mpkt/s", "packets": cnt, "ms_per_batch": round(dt * 1e3, 4),
+                    "avg_kernel_ms": round(float(np.mean(ks)), 4), "mode_used": st["mode_used"], "conflict": st["conflict"]}
+        vm.close()
+    return out
+
+
 def single_process_multi(args, name: str, n: int) -> None:
     """`bench.py --gpus N` without torchrun: one process drives N GPUs through the C ABI
     (xe_multi_create / xe_run_batch_multi: concurrent shards, RCCL delta all-reduce or in-order
@@ -231,6 +262,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", default="auto", choices=["auto", "interp", "jit"])
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
+    ap.add_argument("--no-ordered", action="store_true", help="skip the C2-RMW ordered-path lines (C2 only)")
     args = ap.parse_args()
 
     import torch
@@ -321,6 +353,9 @@ def main() -> None:
     e2e = None
     if rank == 0 and not args.no_e2e:
         e2e = e2e_baseline(vm, umem, descs)
+    ordered = None
+    if rank == 0 and name == "c2" and not args.no_ordered:
+        ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
     del umem
     if rank == 0:
         cpu = None
@@ -357,6 +392,7 @@ def main() -> None:
                          "issue_frac": round(insns_per_pkt * n / avg_kernel_s / ISSUE_PEAK, 5)},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "ordered": ordered,
         }
         print(json.dumps(out), flush=True)
     vm.close()

@@ -60,6 +60,7 @@ enum : uint8_t {
   UF_REG = 2,        // BPF_X form
   UF_BADDST = 4,     // LDX: Assign(dst) will fail after the read (dst > 9)
   UF_BADSRC = 8,     // ATOMIC: Get(src) will fail after the read (src > 9)
+  UF_LIFT = 0x40,    // LDX / STX of a lifted read-modify-write (lift_rmw, xe_runtime.cpp)
 };
 
 struct XeUop {

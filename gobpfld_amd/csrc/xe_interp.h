@@ -1707,6 +1707,10 @@ XE_DEV int64_t ptr_eff(const XeReg& R, int32_t ioff) {
   return XE_T_KIND(R.t) == XE_KIND_FRAMEPTR ? xe_wadd(xe_wadd(XE_FRAME, R.v), ioff) : xe_wadd(R.v, ioff);
 }
 
+// lifted read-modify-writes run as adds only where lanes run concurrently and no register record
+// could show the loaded value
+XE_DEV bool lift_active(const XeParams& P) { return P.mode == XE_MODE_PARALLEL && !P.regs; }
+
 // ---- per-class handlers (exec_uop dispatches; the JIT calls them directly with constant uops)
 XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
   const int d = u.dst, s = u.src;
@@ -1810,7 +1814,9 @@ XE_DEV int uop_ldx(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cms = 
   XE_NILCHK(S);
   if ((cms & XE_CM_IMM) && XE_T_KIND(S.t) == XE_KIND_IMM) return XE_E_NONPTR_LOAD;
   uint32_t kind, oh, al; int64_t v;
-  if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), true, kind, oh, v, al, cms)) return e;
+  // a lifted load's value only reaches memory through the paired store's add: no read footprint
+  const bool track = !((u.fl & UF_LIFT) && lift_active(P));
+  if (int e = mem_read(L, P, S.h, ptr_eff(S, u.tgt), uop_size(u), track, kind, oh, v, al, cms)) return e;
   if (u.fl & UF_BADDST) return XE_E_ASSIGN_REG;
   reg_replace(L, u.dst, kind, oh, v, al);
   return 0;
@@ -1824,7 +1830,26 @@ XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd 
   const XeReg D = reg_get(L, u.dst);
   XE_NILCHK(D);
   if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
-  return mem_write(L, P, D.h, ptr_eff(D, u.tgt), uop_size(u), XE_T_KIND(S.t), S.h, S.v, cmd);
+  const int64_t off = ptr_eff(D, u.tgt);
+  const int size = uop_size(u);
+  if ((cmd & XE_CM_MAPS) && (u.fl & UF_LIFT) && lift_active(P)) {
+    const uint32_t c = xe_h_cls(D.h);
+    if (c == XE_H_ARRAY || c == XE_H_HASH) {
+      XeBMem B;
+      bmem_resolve(L, P, D.h, B);
+      if (B.map) {  // the lifted read-modify-write of a map value: add the addend (lift_rmw)
+        if (int e = bounds(off, size, B.len)) return e;
+        int64_t k = int64_t(u.imm);
+        if (u.x & 0xff) k = reg_get(L, int(u.x & 0xff) - 1).v;
+        if (u.x & 0x100) k = int64_t(0ull - uint64_t(k));
+        fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
+        width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
+        wave_atomic_add_field(L, B.map, true, B.base + off, size, uint64_t(k));
+        return 0;
+      }
+    }
+  }
+  return mem_write(L, P, D.h, off, size, XE_T_KIND(S.t), S.h, S.v, cmd);
 }
 
 XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {

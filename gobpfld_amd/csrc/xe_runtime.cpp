@@ -311,6 +311,68 @@ int translate(const uint64_t* raw, uint32_t n, std::vector<XeUop>& out, std::str
   return XE_OK;
 }
 
+// Read-modify-write lifting. `ldx rX, [rB+o]; add/sub rX, K|rY; stx [rB+o], rX` with rX dead after the
+// store changes map memory exactly as an atomic add of +-K (mod 2^width) would: the only thing the
+// lane keeps from the loaded value is the stored sum. Marking the pair UF_LIFT lets a parallel lane
+// skip the read footprint and add instead of store (uop_ldx / uop_store), so `value->count++` written
+// without an atomic runs in parallel instead of conflicting into the ordered replay. Programs with
+// bpf-to-bpf calls, tail calls or indirect helper calls are left alone (their register flow leaves the
+// program's own CFG). The stx carries the addend: imm = K, x = (rY + 1 or 0) | 0x100 when subtracting.
+void lift_rmw(std::vector<XeUop>& p) {
+  const size_t n = p.size();
+  for (const XeUop& u : p)
+    if (u.cls == U_CALLBPF || u.cls == U_CALLX || (u.cls == U_HELPER && u.imm == 12)) return;
+  std::vector<bool> target(n + 1, false);
+  for (const XeUop& u : p)
+    if ((u.cls == U_JA || u.cls == U_JMP) && int64_t(u.tgt) + 1 >= 0 && size_t(int64_t(u.tgt) + 1) <= n) target[size_t(u.tgt + 1)] = true;
+  // backward liveness over R0..R10 (bit r); exit reads R0, helpers read R1..R5 and define nothing
+  std::vector<uint16_t> live(n + 1, 0);
+  auto bit = [](int r) { return uint16_t(r >= 0 && r <= 10 ? 1u << r : 0u); };
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (size_t k = n; k-- > 0;) {
+      const XeUop& u = p[k];
+      auto at = [&](int64_t t) -> uint16_t { return t >= 0 && size_t(t) < n ? live[size_t(t)] : 0; };
+      uint16_t out = 0, use = 0, def = 0;
+      switch (u.cls) {
+        case U_EXIT: case U_FAIL: break;
+        case U_JA: out = at(int64_t(u.tgt) + 1); break;
+        case U_JMP: out = uint16_t(at(int64_t(u.tgt) + 1) | at(int64_t(k) + 1)); break;
+        default: out = at(int64_t(k) + 1); break;
+      }
+      switch (u.cls) {
+        case U_EXIT: use = bit(0); break;
+        case U_ALU: use = uint16_t(bit(u.dst) | ((u.fl & UF_REG) ? bit(u.src) : 0)); def = bit(u.dst); break;
+        case U_MOVI: case U_LDIMM64: def = bit(u.dst); break;
+        case U_MOVR: use = bit(u.src); def = bit(u.dst); break;
+        case U_NEG: case U_END: use = def = bit(u.dst); break;
+        case U_LDX: use = bit(u.src); if (!(u.fl & UF_BADDST)) def = bit(u.dst); break;
+        case U_ST: use = bit(u.dst); break;
+        case U_STX: case U_ATOMIC: use = uint16_t(bit(u.dst) | bit(u.src)); break;
+        case U_JMP: use = uint16_t(bit(u.dst) | ((u.fl & UF_REG) ? bit(u.src) : 0)); break;
+        case U_HELPER: use = 0x3e; break;
+        default: break;
+      }
+      const uint16_t in = uint16_t(use | (out & ~def));
+      if (in != live[k]) { live[k] = in; changed = true; }
+    }
+  }
+  for (size_t k = 0; k + 2 < n; k++) {
+    XeUop &l = p[k], &a = p[k + 1], &s = p[k + 2];
+    if (l.cls != U_LDX || (l.fl & UF_BADDST) || a.cls != U_ALU || s.cls != U_STX) continue;
+    const int w = uop_size(l);
+    const int rx = l.dst, rb = l.src;
+    if ((w != 4 && w != 8) || rx == rb || target[k + 1] || target[k + 2]) continue;
+    if (a.dst != rx || (a.x != 0x00 && a.x != 0x10) || ((a.fl & UF_REG) && a.src == rx) || (w == 8 && !(a.fl & UF_WIDE))) continue;
+    if (s.dst != rb || s.src != rx || s.tgt != l.tgt || uop_size(s) != w) continue;
+    if (k + 3 < n && (live[k + 3] & bit(rx))) continue;
+    l.fl |= UF_LIFT;
+    s.fl |= UF_LIFT;
+    s.imm = (a.fl & UF_REG) ? 0 : a.imm;
+    s.x = ((a.fl & UF_REG) ? uint32_t(a.src) + 1u : 0u) | (a.x == 0x10 ? 0x100u : 0u);
+  }
+}
+
 // ------------------------------------------------------------------ maps
 uint32_t next_pow2(uint64_t v) {
   uint32_t p = 16;
@@ -917,6 +979,7 @@ int xe_add_raw_program(xe_vm* vm, const uint64_t* insns, uint32_t n, int32_t* id
   std::string err;
   int rc = translate(insns, n, prog, err);
   if (rc) return fail(vm, rc, err);
+  lift_rmw(prog);
   vm->programs.push_back(std::move(prog));
   if (idx) *idx = int32_t(vm->programs.size() - 1);
   return XE_OK;
@@ -1744,6 +1807,7 @@ int xe_translate_uops(const uint64_t* insns, uint32_t n, void* out, uint32_t cap
   std::string err;
   int rc = translate(insns, n, prog, err);
   if (rc) return rc;
+  lift_rmw(prog);
   if (out && cap >= prog.size()) memcpy(out, prog.data(), prog.size() * sizeof(XeUop));
   return int(prog.size());
 }

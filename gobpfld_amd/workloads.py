@@ -72,8 +72,10 @@ def _parse_eth(a: Asm, drop: str) -> None:
     a.label("novlan")
 
 
-def prog_c2() -> list[int]:
-    """L2/L3 classifier: proto of IPv4/IPv6, count per proto in ARRAY map 1, PASS TCP/UDP/ICMP."""
+def prog_c2(rmw: bool = False) -> list[int]:
+    """L2/L3 classifier: proto of IPv4/IPv6, count per proto in ARRAY map 1, PASS TCP/UDP/ICMP.
+    rmw: the counter is bumped the way `value->packets++` compiles without __sync_fetch_and_add
+    (load, add, store: an ordered read-modify-write unless lifted, xe_runtime.cpp lift_rmw)."""
     a = Asm()
     _parse_eth(a, "drop")
     a.jmp(JEQ, 3, "ipv4", imm=0x0008)      # 0x0800
@@ -96,8 +98,11 @@ def prog_c2() -> list[int]:
     a.mov64(2, src=10).add64(2, -4)
     a.call(1)                              # bpf_map_lookup_elem
     a.jmp(JEQ, 0, "verdict", imm=0)        # NULL (IMM 0) -> skip; a pointer never compares
-    a.mov64(1, 1)
-    a.xadd(8, 0, 0, 1)                     # lock *(u64 *)(r0 + 0) += 1
+    if rmw:
+        a.ldx(8, 1, 0, 0).add64(1, 1).stx(8, 0, 0, 1)  # *(u64 *)(r0 + 0) += 1, not atomic
+    else:
+        a.mov64(1, 1)
+        a.xadd(8, 0, 0, 1)                 # lock *(u64 *)(r0 + 0) += 1
     a.label("verdict")
     a.mov64(0, XDP_PASS)
     a.jmp(JEQ, 8, "out", imm=6)            # TCP
@@ -391,6 +396,7 @@ def c5_map_entries() -> tuple[np.ndarray, np.ndarray]:
 CONFIGS = {
     "c1": dict(program=prog_c1, pkt=64, n=1024),
     "c2": dict(program=prog_c2, pkt=64, n=16 * 1024 * 1024),
+    "c2rmw": dict(program=lambda: prog_c2(rmw=True), pkt=64, n=16 * 1024 * 1024),
     "c3": dict(program=prog_c3, pkt="imix", n=16 * 1024 * 1024),
     "c4": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024),
     "c5": dict(program=prog_c5, pkt=64, n=256 * 1024 * 1024),
@@ -398,7 +404,7 @@ CONFIGS = {
 
 
 def workload_maps(name: str) -> list[tuple[MapDef, tuple[np.ndarray, np.ndarray] | None]]:
-    if name == "c2":
+    if name in ("c2", "c2rmw"):
         return [(MapDef(MAP_ARRAY, 4, 8, 256), None)]
     if name == "c3":
         return [(MapDef(MAP_HASH, 16, 16, C3_MAX), c3_map_entries())]
@@ -414,7 +420,7 @@ def headers(name: str, idx: np.ndarray, hdr: int = 64) -> np.ndarray:
         for b in range(hdr):
             h[:, b] = (r >> np.uint64(8 * (b % 8))) & np.uint64(0xFF)
         return h
-    return {"c2": headers_c2, "c3": headers_c3, "c4": headers_c4, "c5": headers_c5}[name](idx, hdr)
+    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c4": headers_c4, "c5": headers_c5}[name](idx, hdr)
 
 
 def packet_sizes(name: str, idx: np.ndarray) -> np.ndarray:

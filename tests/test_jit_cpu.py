@@ -27,7 +27,7 @@ def _uops(lib, raw):
     return out, n
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c2rmw", "c3", "c4", "c5"])
 def test_config_kernel_compiles(prod, name):
     u, n = _uops(prod, W.CONFIGS[name]["program"]())
     log = C.create_string_buffer(4096)

@@ -1144,11 +1144,86 @@ XE_DEV void hash_set_state(const XeDevMap& M, uint64_t slot, uint32_t st) {
 
 // Linear probing over slot records: the state word and the key words of a record are loaded
 // together (independent loads of one line), then compared. LRU maps leave tombstones behind evictions.
+//
+// When the record geometry is a compile-time constant (per-program kernels), one probe step loads
+// every record from the probe position to the end of its XE_PROBE_GROUP-byte group at once and then
+// scans them in slot order: the same first-match / stop-at-empty walk as one record at a time, but a
+// chain that stays inside a cache line costs one memory round trip instead of one per record.
+#ifndef XE_PROBE_GROUP
+#define XE_PROBE_GROUP 64
+#endif
+#if defined(__HIPCC__) && XE_PROBE_GROUP
+XE_DEV void xe_group_load(XE_GP(const uint64_t) p, uint64_t* w) {
+  static_assert(XE_PROBE_GROUP == 64 || XE_PROBE_GROUP == 128, "probe group: 64 or 128 bytes");
+  xe_u4 a[XE_PROBE_GROUP / 16];
+#if XE_PROBE_GROUP == 64
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %4, off offset:16\n\t"
+      "global_load_dwordx4 %2, %4, off offset:32\n\tglobal_load_dwordx4 %3, %4, off offset:48\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3])
+      : "v"(p));
+#else
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off\n\tglobal_load_dwordx4 %1, %8, off offset:16\n\t"
+      "global_load_dwordx4 %2, %8, off offset:32\n\tglobal_load_dwordx4 %3, %8, off offset:48\n\t"
+      "global_load_dwordx4 %4, %8, off offset:64\n\tglobal_load_dwordx4 %5, %8, off offset:80\n\t"
+      "global_load_dwordx4 %6, %8, off offset:96\n\tglobal_load_dwordx4 %7, %8, off offset:112\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(a[6]), "=&v"(a[7])
+      : "v"(p));
+#endif
+#pragma unroll
+  for (int j = 0; j < XE_PROBE_GROUP / 8; j++)
+    w[j] = uint64_t(a[j >> 1][2 * (j & 1)]) | (uint64_t(a[j >> 1][2 * (j & 1) + 1]) << 32);
+}
+#endif
 XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
   if (empty) return (hash_state(M, M.cap) & XE_SLOT_FULL) ? int64_t(M.cap) : -1;
   uint64_t hv = xe_hash_words(kw, M.kwords, M.key_size);
   uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(hv) & mask;
+#if defined(__HIPCC__) && XE_PROBE_GROUP
+  if (__builtin_constant_p(M.rwords) && __builtin_constant_p(M.kwords) && __builtin_constant_p(M.cap) &&
+      M.rwords * 8 < XE_PROBE_GROUP && M.cap >= XE_PROBE_GROUP / (M.rwords * 8)) {
+    constexpr uint32_t kMaxG = XE_PROBE_GROUP / 8;  // records per group for 1-word records
+    static_assert(kMaxG <= 32, "hit / stop masks");
+    const uint32_t G = XE_PROBE_GROUP / (M.rwords * 8);
+#pragma unroll 1
+    for (uint32_t probe = 0; probe < M.cap;) {
+      const uint32_t first = idx & (G - 1);
+      XE_GP(const uint64_t) r = (XE_GP(const uint64_t))M.keys + uint64_t(idx - first) * M.rwords;
+      // the whole group (it lies inside the record array: cap is a multiple of G) in one burst of
+      // 16-byte loads with a single wait: the compiler would otherwise interleave each record's load
+      // with its compare under register pressure, one round trip per record again
+      uint64_t w[XE_PROBE_GROUP / 8];
+      xe_group_load(r, w);
+      // branch-free scan (a compare under a branch would let the compiler sink its load behind the
+      // other records' wait): bit g of hit / stop = record g matches / ends the chain
+      uint32_t hit = 0, stop = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < kMaxG; g++) {
+        if (g >= G) continue;
+        const uint32_t st = uint32_t(w[g * M.rwords]);
+        const bool full = (st & XE_SLOT_FULL) != 0;
+        bool eq = true;
+#pragma unroll
+        for (uint32_t k = 0; k < XE_MAX_KEY / 8; k++)
+          if (k < M.kwords) eq = eq && (w[g * M.rwords + k + 1] == kw[k]);
+        hit |= uint32_t(full && eq) << g;
+        stop |= uint32_t(!full && !(XE_HAS_ORDERED && (st & XE_SLOT_TOMB))) << g;
+      }
+      const uint32_t act = (hit | stop) & (~0u << first);
+      if (act) {
+        const uint32_t g0 = uint32_t(__builtin_ctz(act));
+        return ((hit >> g0) & 1u) ? int64_t(idx - first + g0) : -1;
+      }
+      probe += G - first;
+      idx = (idx - first + G) & mask;
+    }
+    return -1;
+  }
+#endif
 #pragma unroll 1
   for (uint32_t probe = 0; probe < M.cap; probe++) {
     XE_GP(const uint64_t) r = (XE_GP(const uint64_t))M.keys + uint64_t(idx) * M.rwords;

@@ -82,6 +82,8 @@ _SIGS = {
     "run_batch": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),  # oracle form
     "run_batch_host": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P]),
     "run_batch_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
+    "run_batch_device_async": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
+    "sync": (C.c_int, [P]),
     "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
     "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
@@ -112,7 +114,7 @@ HEADER_SYMBOLS = [
     "xe_default_settings", "xe_create", "xe_destroy", "xe_last_error", "xe_add_raw_program",
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
     "xe_map_count", "xe_map_dump", "xe_map_dump_list", "xe_map_lru_order", "xe_map_push", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
-    "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
+    "xe_run_batch_device_async", "xe_sync", "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
     "xe_device_count", "xe_shard_check", "xe_map_state_bytes", "xe_map_state_export", "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error",
 ]

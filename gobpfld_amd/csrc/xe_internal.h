@@ -225,4 +225,11 @@ struct XeParams {
   uint32_t nprogs;          // len(vm.Programs) - 1
   int32_t entry;            // PI at Reset (SetEntrypoint)
   XeGen gen;
+  // pipelined batches (xe_run_batch_device_async): set on the device by an earlier batch's epilogue
+  // when that batch must be replayed in order; the launch then does nothing (null: synchronous run)
+  const uint32_t* poison;
 };
+
+// Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in
+// packet order (same rule as the synchronous run's conflict check)
+#define XE_AUX_DECISION 1

@@ -2255,6 +2255,8 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   const uint32_t nchunks = (P.n + (XE_WAVE - 1)) / XE_WAVE;
   uint32_t c = wave;
   if (c >= nchunks) return;
+  // an earlier pipelined batch is being replayed in order: this one re-runs afterwards
+  if (P.poison && xe_readfirst(int(xe_load_relaxed32(const_cast<unsigned int*>(P.poison))))) return;
   uint32_t i0 = c * XE_WAVE + lane;
   bool v0 = i0 < P.n;
   uint64_t a0;

@@ -84,7 +84,42 @@ extern "C" __global__ void xe_prologue_kernel(XeProlog A) {
     for (uint64_t i = tid; i < A.words[g]; i += nth) A.dst[g][i] = A.src[g][i];
 }
 
+// Pipelined-batch epilogue (xe_run_batch_device_async): the synchronous run's conflict rule evaluated
+// on the device, so the next batch, already queued behind this one, knows before it starts whether
+// this batch will be replayed in order. One block: thread w ORs word w of the per-wave records over
+// the replicas, thread 0 decides; a replay sets the poison word (the next launches do nothing) and
+// aux[XE_AUX_DECISION]. Layout of aux: xe_runtime.cpp (read_aux / reduce).
+extern "C" __global__ void __launch_bounds__(256) xe_epilogue_kernel(unsigned long long* aux, uint32_t nrep, uint32_t rep_words,
+                                                                     uint32_t nmaps, uint32_t mode, uint32_t* poison) {
+  __shared__ unsigned long long orw[256];
+  const uint32_t t = threadIdx.x;
+  unsigned long long o = 0;
+  if (t < rep_words)
+    for (uint32_t r = 0; r < nrep; r++) o |= aux[16 + uint64_t(r) * rep_words + t];
+  orw[t] = o;
+  __syncthreads();
+  if (t != 0) return;
+  if (*poison) return;  // this batch did not run: an earlier one is being replayed
+  const uint32_t flags = uint32_t(aux[0]);
+  bool conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
+  for (uint32_t m = 1; m <= nmaps && m < 64 && 17 + 2 * m < 256; m++) {
+    if (orw[16 + 2 * m] & orw[16 + 2 * m + 1]) conflict = true;
+    const unsigned wc = unsigned(orw[XE_REC_WIDTH0 + m / 16] >> (4 * (m % 16))) & 15u;
+    if (wc & (wc - 1)) conflict = true;
+  }
+  const bool replay = conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY));
+  aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
+  if (replay) *poison = 1u;
+}
+
 // host-side launchers (called from xe_runtime.cpp)
+extern "C" int xe_launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison,
+                                  hipStream_t s) {
+  if (rep_words > 256) return -1;
+  hipLaunchKernelGGL(xe_epilogue_kernel, dim3(1), dim3(256), 0, s, (unsigned long long*)aux, nrep, rep_words, nmaps, mode,
+                     (uint32_t*)poison);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
   hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;

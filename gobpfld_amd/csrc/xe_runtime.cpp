@@ -33,6 +33,8 @@ extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, 
 extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
+extern "C" int xe_launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison,
+                                  hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
                             bool* general, const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -120,10 +122,31 @@ int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t 
     for (uint32_t k = 0; k < nrep; k++) { v[i] += r[k * sw + i]; r[k * sw + i] = 0; }
   return 0;
 }
+int launch_epilogue(void* auxp, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison, xe_stream_t) {
+  unsigned long long* aux = (unsigned long long*)auxp;
+  std::vector<unsigned long long> orw(rep_words, 0);
+  for (uint32_t t = 0; t < rep_words; t++)
+    for (uint32_t r = 0; r < nrep; r++) orw[t] |= aux[16 + uint64_t(r) * rep_words + t];
+  if (*(uint32_t*)poison) return 0;
+  const uint32_t flags = uint32_t(aux[0]);
+  bool conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
+  for (uint32_t m = 1; m <= nmaps && m < 64; m++) {
+    if (orw[16 + 2 * m] & orw[16 + 2 * m + 1]) conflict = true;
+    const unsigned wc = unsigned(orw[XE_REC_WIDTH0 + m / 16] >> (4 * (m % 16))) & 15u;
+    if (wc & (wc - 1)) conflict = true;
+  }
+  const bool replay = conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY));
+  aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
+  if (replay) *(uint32_t*)poison = 1u;
+  return 0;
+}
+int host_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
+void host_free(void* p) { free(p); }
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
   static float ms(const Timer& a, const Timer& b) { return std::chrono::duration<float, std::milli>(b.t - a.t).count(); }
+  int wait() { return 0; }
   void init() {}
   void fini() {}
 };
@@ -154,11 +177,17 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
                     xe_stream_t s) {
   return xe_launch_prologue(src, dst, words, nseg, zero, zw, s);
 }
+int launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison, xe_stream_t s) {
+  return xe_launch_epilogue(aux, nrep, rep_words, nmaps, mode, poison, s);
+}
+int host_alloc(void** p, size_t n) { return hipHostMalloc(p, n ? n : 8, hipHostMallocDefault) == hipSuccess ? 0 : -1; }
+void host_free(void* p) { if (p) (void)hipHostFree(p); }
 struct Timer {
   hipEvent_t e = nullptr;
   void init() { if (!e) (void)hipEventCreate(&e); }
   void fini() { if (e) (void)hipEventDestroy(e); e = nullptr; }
   void rec(xe_stream_t s) { init(); (void)hipEventRecord(e, s); }
+  int wait() { return hipEventSynchronize(e) == hipSuccess ? 0 : -1; }
   static float ms(const Timer& a, const Timer& b) { float m = 0; (void)hipEventElapsedTime(&m, a.e, b.e); return m; }
 };
 int set_device(int d) { return hipSetDevice(d) == hipSuccess ? 0 : -1; }
@@ -380,6 +409,8 @@ uint32_t next_pow2(uint64_t v) {
   return p;
 }
 
+constexpr uint32_t kAsyncDepth = 3;  // pipelined batches in flight per VM (xe_run_batch_device_async)
+
 struct HostMap {
   xe_map_def def{};
   uint32_t dkind = XE_DM_NONE;
@@ -394,6 +425,7 @@ struct HostMap {
   uint32_t* d_state = nullptr;
   uint32_t* d_count = nullptr;
   uint8_t* d_snap = nullptr;
+  std::array<uint8_t*, kAsyncDepth> d_asnap{};  // rollback points of the pipelined batches in flight
   uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
   uint32_t nrep = 1;
   uint64_t rep_stride = 0;
@@ -522,6 +554,28 @@ struct xe_vm {
   // room the ordered maps' device copies keep for one run (elements / events, event bytes), grown
   // ×4 when a run reports XE_FLAG_CAPACITY
   uint64_t ord_slack = 4096, ord_slack_bytes = 1 << 20;
+  // pipelined batches (xe_run_batch_device_async): a ring of slots, each with its own statistics /
+  // footprint buffer (device + pinned host copy), events and map rollback points; `pending` holds the
+  // slots in flight in submission order. d_poison: set by an epilogue whose batch must be replayed.
+  struct Batch {
+    void* d_umem = nullptr; uint64_t umem_len = 0; const void* d_desc = nullptr; uint32_t n = 0;
+    void* d_results = nullptr; void* d_verdicts = nullptr; void* d_regs = nullptr;
+    xe_stream_t s = nullptr; xe_batch_stats* stats = nullptr;
+  };
+  struct Slot {
+    unsigned long long* d_aux = nullptr;
+    unsigned long long* h_aux = nullptr;
+    Timer t0, t1, done;
+    Batch b;
+    size_t aux_used = 0;
+    uint32_t nmaps = 0, grid = 0, engine = 0;
+  };
+  std::array<Slot, kAsyncDepth> slots;
+  std::vector<uint32_t> pending;
+  uint32_t next_slot = 0;
+  uint32_t* d_poison = nullptr;
+  bool draining = false;
+  bool delta_base = true;  // the map snapshots are the start of the last batch (false after async batches)
 };
 
 namespace {
@@ -574,6 +628,7 @@ int map_alloc_device(HostMap& m) {
 }
 
 void map_free_device(HostMap& m) {
+  for (auto& p : m.d_asnap) { dev_free(p); p = nullptr; }
   dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count); dev_free(m.d_rep);
   m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr; m.d_rep = nullptr;
   dev_free(m.d_hdr); dev_free(m.d_link); dev_free(m.d_elen); dev_free(m.d_rec);
@@ -788,6 +843,7 @@ void lru_promote_host(HostMap& m, size_t i) {
 
 HostMap* get_map(xe_vm* vm, int32_t idx) {
   if (!vm || idx < 1 || idx >= int32_t(vm->maps.size())) return nullptr;
+  if (!vm->pending.empty() && xe_sync(vm)) return nullptr;  // map state after every pipelined batch
   return &vm->maps[idx];
 }
 
@@ -959,6 +1015,13 @@ int xe_create(const xe_settings* s, xe_vm** out) {
 void xe_destroy(xe_vm* vm) {
   if (!vm) return;
   set_device(vm->settings.device);
+  for (uint32_t si : vm->pending) (void)vm->slots[si].done.wait();  // no launch may outlive its buffers
+  vm->pending.clear();
+  for (auto& sl : vm->slots) {
+    dev_free(sl.d_aux); host_free(sl.h_aux);
+    sl.t0.fini(); sl.t1.fini(); sl.done.fini();
+  }
+  dev_free(vm->d_poison);
   for (auto& m : vm->maps) map_free_device(m);
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
@@ -975,6 +1038,7 @@ const char* xe_last_error(const xe_vm* vm) { return vm ? vm->last_error.c_str() 
 
 int xe_add_raw_program(xe_vm* vm, const uint64_t* insns, uint32_t n, int32_t* idx) {
   if (!vm || (!insns && n)) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;  // a replay of a pipelined batch must see the VM it was queued on
   std::vector<XeUop> prog;
   std::string err;
   int rc = translate(insns, n, prog, err);
@@ -987,6 +1051,7 @@ int xe_add_raw_program(xe_vm* vm, const uint64_t* insns, uint32_t n, int32_t* id
 
 int xe_set_entrypoint(xe_vm* vm, int32_t idx) {  // emulator/vm.go:100-108
   if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
   if (idx < 1 || int32_t(vm->programs.size()) <= idx) return fail(vm, XE_ERR_INVAL, "program index out of bounds");
   vm->entry = idx;
   return XE_OK;
@@ -994,6 +1059,7 @@ int xe_set_entrypoint(xe_vm* vm, int32_t idx) {  // emulator/vm.go:100-108
 
 int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_len, int32_t* idx) {
   if (!vm || !def) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
   if (vm->maps.size() > XE_H_MAX_MAPS) return fail(vm, XE_ERR_UNSUPPORTED, "at most 63 maps");
   HostMap m;
   m.def = *def;
@@ -1356,14 +1422,11 @@ static int ensure_arena(xe_vm* vm, bool seq, uint32_t nl, XeGen& g) {
   return 0;
 }
 
-int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
-                        void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
-  if (!vm) return XE_ERR_INVAL;
-  if (stats) memset(stats, 0, sizeof *stats);
-  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
-  if (int rc = prepare_run(vm, s)) return rc;
-  if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
+namespace {
 
+// launch parameters of a batch (flags / replica records at aux)
+XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n, void* d_results,
+                      void* d_verdicts, void* d_regs, unsigned long long* aux) {
   XeParams P{};
   P.progs = vm->d_progs;
   P.prog_off = vm->d_prog_off;
@@ -1384,17 +1447,20 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   P.max_steps = vm->settings.max_steps;
   P.ingress = vm->settings.ingress_ifindex;
   P.rxq = vm->settings.rx_queue_index;
-  P.flags = reinterpret_cast<uint32_t*>(vm->d_aux);
-  P.rep = vm->d_aux + 16;
+  P.flags = reinterpret_cast<uint32_t*>(aux);
+  P.rep = aux + 16;
   P.nrep = kRep;
   P.rep_words = 16 + 2 * (P.nmaps + 1);
-  const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+  return P;
+}
 
-  const uint32_t mode = vm->settings.mode;
-  const uint32_t engine = vm->settings.engine;
-  void* jit = nullptr;
-  bool jit_general = false;
+// The kernel a batch runs: the per-program kernel (compiled on first use for this program and map
+// geometry) unless the settings or the program need the interpreter.
+int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
+  jit = nullptr;
+  jit_general = false;
 #ifndef XE_HOSTSIM
+  const uint32_t engine = vm->settings.engine;
   if (engine != XE_ENGINE_INTERP && jit_possible(vm)) {
     if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size()) {
       // the kernel is specialised on the program and the map geometry (xe_jit.cpp)
@@ -1416,6 +1482,79 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   }
   if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
 #endif
+  return XE_OK;
+}
+
+// parallel-mode grid for the selected kernel (resident blocks; the general model's arena bounds it)
+uint32_t parallel_grid(xe_vm* vm, void* jit, bool general, uint32_t n, uint32_t nmaps) {
+  if (vm->cus < 0) vm->cus = cu_count(vm->settings.device);
+  int& occ = jit ? vm->occ_jit : vm->occ_interp;
+  if ((jit && jit != vm->occ_jit_fn) || nmaps != vm->occ_nmaps) {
+    vm->occ_jit_fn = jit ? jit : vm->occ_jit_fn;
+    vm->occ_nmaps = nmaps;
+    vm->occ_jit = vm->occ_interp = -1;
+  }
+  if (occ < 0) occ = blocks_per_cu(jit, nmaps);
+  uint32_t g = grid_blocks(n, occ, vm->cus);
+  if (general) g = std::min<uint32_t>(g, 512);  // bounds the per-lane arena
+  return g;
+}
+
+// sum / OR the per-wave replica records: red[0] flags, [1] steps, [2..9] status histogram,
+// [XE_REC_WIDTH0 + 2 + k] width classes, [16 + 2m] / [17 + 2m] read / atomic masks of map m
+void reduce_aux(const unsigned long long* aux, uint32_t nmaps, uint32_t rep_words, std::vector<unsigned long long>& red) {
+  red.assign(16 + 2 * size_t(nmaps + 1), 0);
+  red[0] = aux[0];
+  for (uint32_t r = 0; r < kRep; r++) {
+    const unsigned long long* rec = aux + 16 + size_t(r) * rep_words;
+    red[1] += rec[0];
+    for (int k = 0; k < 8; k++) red[2 + k] += rec[1 + k];
+    for (int k = 0; k < 4; k++) red[XE_REC_WIDTH0 + 2 + k] |= rec[XE_REC_WIDTH0 + k];
+    for (uint32_t w = 0; w < 2 * (nmaps + 1); w++) red[16 + w] |= rec[16 + w];
+  }
+}
+
+// order-dependent map effects in a parallel run: an ordered write or a lane out of arena, a read of
+// a field other lanes add to, or adds of more than one width on a map (a narrow add's carry stops
+// at its own top byte)
+bool run_conflict(const std::vector<unsigned long long>& red, uint32_t nmaps) {
+  bool conflict = (uint32_t(red[0]) & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
+  for (uint32_t m = 1; m <= nmaps && m < 64; m++) {
+    if (red[16 + 2 * m] & red[16 + 2 * m + 1]) conflict = true;
+    const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
+    if (wc & (wc - 1)) conflict = true;
+  }
+  return conflict;
+}
+
+// per-map add widths of the last run (the lanes of the cross-shard deltas)
+void record_widths(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t nmaps) {
+  for (uint32_t m = 1; m <= nmaps && m < 64; m++) {
+    const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
+    vm->maps[m].wclass = wc;
+    vm->maps[m].lane = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
+  }
+}
+
+}  // namespace
+
+int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
+                        void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
+  if (!vm) return XE_ERR_INVAL;
+  if (stats) memset(stats, 0, sizeof *stats);
+  if (int rc = xe_sync(vm)) return rc;  // pipelined batches first: they precede this one
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (int rc = prepare_run(vm, s)) return rc;
+  if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
+  vm->delta_base = true;
+
+  XeParams P = batch_params(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, vm->d_aux);
+  const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+
+  const uint32_t mode = vm->settings.mode;
+  void* jit = nullptr;
+  bool jit_general = false;
+  if (int rc = select_engine(vm, jit, jit_general)) return rc;
   const bool general = !jit || jit_general;  // lanes keep their state in the XeGen arena
   auto launch = [&](const XeParams* p, uint32_t b, uint32_t t) {
     return jit ? launch_jit(jit, p, b, t, s) : launch_interp(p, b, t, s);
@@ -1443,17 +1582,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   std::vector<unsigned long long> aux(aux_used);
   std::vector<unsigned long long> red;
   // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
-  auto reduce = [&]() {
-    red.assign(16 + 2 * size_t(P.nmaps + 1), 0);
-    red[0] = aux[0];
-    for (uint32_t r = 0; r < kRep; r++) {
-      const unsigned long long* rec = aux.data() + 16 + size_t(r) * P.rep_words;
-      red[1] += rec[0];
-      for (int k = 0; k < 8; k++) red[2 + k] += rec[1 + k];
-      for (int k = 0; k < 4; k++) red[XE_REC_WIDTH0 + 2 + k] |= rec[XE_REC_WIDTH0 + k];
-      for (uint32_t w = 0; w < 2 * (P.nmaps + 1); w++) red[16 + w] |= rec[16 + w];
-    }
-  };
+  auto reduce = [&]() { reduce_aux(aux.data(), P.nmaps, P.rep_words, red); };
   auto read_aux = [&]() -> int {
     if (d2h(aux.data(), vm->d_aux, aux_used * 8, s) || dsync(s)) return -1;
     reduce();
@@ -1527,19 +1656,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (int rc = sequential(kms)) return rc;
   } else {
     P.mode = XE_MODE_PARALLEL;
-    if (vm->cus < 0) vm->cus = cu_count(vm->settings.device);
-    int& occ = jit ? vm->occ_jit : vm->occ_interp;
-    if ((jit && jit != vm->occ_jit_fn) || P.nmaps != vm->occ_nmaps) {
-      vm->occ_jit_fn = jit ? jit : vm->occ_jit_fn;
-      vm->occ_nmaps = P.nmaps;
-      vm->occ_jit = vm->occ_interp = -1;
-    }
-    if (occ < 0) occ = blocks_per_cu(jit, P.nmaps);
-    vm->last_grid = grid_blocks(n, occ, vm->cus);
-    if (general) {
-      vm->last_grid = std::min<uint32_t>(vm->last_grid, 512);  // bounds the per-lane arena
-      if (ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
-    }
+    vm->last_grid = parallel_grid(vm, jit, general, n, P.nmaps);
+    if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
     vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
     // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
@@ -1551,13 +1669,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
     kms = Timer::ms(vm->t0, vm->t1);
     const uint32_t flags = uint32_t(red[0]);
-    conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
-    for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
-      if (red[16 + 2 * m] & red[16 + 2 * m + 1]) conflict = true;
-      // atomic adds of more than one width on a map do not commute (carry stops at a field's top)
-      const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
-      if (wc & (wc - 1)) conflict = true;
-    }
+    conflict = run_conflict(red, P.nmaps);
     if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
       // order-dependent batch (or a lane out of arena): roll the maps back and replay in packet order
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
@@ -1565,11 +1677,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (int rc = sequential(kms)) return rc;
     }
   }
-  for (uint32_t m = 1; m <= P.nmaps && m < 64; m++) {
-    const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
-    vm->maps[m].wclass = wc;
-    vm->maps[m].lane = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
-  }
+  record_widths(vm, red, P.nmaps);
   if (used == XE_MODE_SEQUENTIAL) {
     // in-program inserts change the entry count: refresh the replica-sizing hint
     std::vector<uint32_t> counts(vm->maps.size(), 0);
@@ -1594,6 +1702,146 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     stats->engine_used = jit ? XE_ENGINE_JIT : XE_ENGINE_INTERP;
     stats->grid_blocks = used == XE_MODE_PARALLEL ? vm->last_grid : 1;
   }
+  return XE_OK;
+}
+
+namespace {
+
+// Complete the oldest pipelined batch: wait for its read-back, then publish its statistics, or — when
+// its epilogue decided on an in-order replay — roll the maps back to its start and re-run it and every
+// later batch (they did nothing on the device) through the synchronous path, in submission order.
+int complete_oldest(xe_vm* vm) {
+  const uint32_t si = vm->pending.front();
+  xe_vm::Slot& sl = vm->slots[si];
+  if (sl.done.wait()) {
+    vm->pending.clear();
+    return fail(vm, XE_ERR_DEVICE, "kernel failed (pipelined batch)");
+  }
+  const unsigned long long* aux = sl.h_aux;
+  if (aux[XE_AUX_DECISION]) {
+    const xe_stream_t s = sl.b.s;
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (!m.ordered() && d2d(m.d_vals, m.d_asnap[si], m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+    }
+    if (dmemset(vm->d_poison, 0, 4, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+    std::vector<xe_vm::Batch> redo;
+    for (uint32_t k : vm->pending) redo.push_back(vm->slots[k].b);
+    vm->pending.clear();
+    for (const xe_vm::Batch& b : redo)
+      if (int rc = xe_run_batch_device(vm, b.d_umem, b.umem_len, b.d_desc, b.n, b.d_results, b.d_verdicts, b.d_regs, b.s,
+                                       b.stats))
+        return rc;
+    return XE_OK;
+  }
+  std::vector<unsigned long long> red;
+  reduce_aux(aux, sl.nmaps, 16 + 2 * (sl.nmaps + 1), red);
+  record_widths(vm, red, sl.nmaps);
+  vm->last_flags = uint32_t(red[0]);
+  vm->last_mode = XE_MODE_PARALLEL;
+  vm->last_fp.assign(red.begin() + 16, red.end());
+  if (xe_batch_stats* st = sl.b.stats) {
+    st->packets = sl.b.n;
+    st->steps = red[1];
+    for (int k = 0; k < 8; k++) st->status_count[k] = red[2 + k];
+    st->mode_used = XE_MODE_PARALLEL;
+    st->conflict = run_conflict(red, sl.nmaps) ? 1 : 0;  // reported, not replayed (XE_MODE_PARALLEL)
+    st->kernel_ms = Timer::ms(sl.t0, sl.t1);
+    st->total_ms = st->kernel_ms;
+    st->engine_used = sl.engine;
+    st->grid_blocks = sl.grid;
+  }
+  vm->pending.erase(vm->pending.begin());
+  return XE_OK;
+}
+
+}  // namespace
+
+int xe_sync(xe_vm* vm) {
+  if (!vm) return XE_ERR_INVAL;
+  while (!vm->pending.empty())
+    if (int rc = complete_oldest(vm)) {
+      vm->pending.clear();
+      return rc;
+    }
+  return XE_OK;
+}
+
+int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
+                              void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
+  if (!vm) return XE_ERR_INVAL;
+  if (stats) memset(stats, 0, sizeof *stats);
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  const bool entry_ok = vm->entry >= 1 && vm->entry < int32_t(vm->programs.size());
+  // batches that cannot pipeline run synchronously, after everything in flight
+  if (!entry_ok || vm->settings.mode == XE_MODE_SEQUENTIAL || has_ordered_maps(vm) ||
+      (umem_len && may_write_packet(vm->programs[vm->entry])))
+    return xe_run_batch_device(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, stream, stats);
+  if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
+  // the pipeline is stream order: a batch on another stream waits for the ones in flight
+  if (!vm->pending.empty() && vm->slots[vm->pending.back()].b.s != s)
+    if (int rc = xe_sync(vm)) return rc;
+  while (vm->pending.size() >= kAsyncDepth)
+    if (int rc = complete_oldest(vm)) {
+      vm->pending.clear();
+      return rc;
+    }
+  if (int rc = prepare_run(vm, s)) return rc;
+  void* jit = nullptr;
+  bool jit_general = false;
+  if (int rc = select_engine(vm, jit, jit_general)) return rc;
+  const bool general = !jit || jit_general;
+
+  const uint32_t si = vm->next_slot;
+  xe_vm::Slot& sl = vm->slots[si];
+  if ((!sl.d_aux && dev_alloc((void**)&sl.d_aux, kAuxWords * 8)) || (!sl.h_aux && host_alloc((void**)&sl.h_aux, kAuxWords * 8)))
+    return fail(vm, XE_ERR_DEVICE, "alloc (pipelined batch records)");
+  if (!vm->d_poison) {
+    if (dev_alloc((void**)&vm->d_poison, 8) || dmemset(vm->d_poison, 0, 8, s)) return fail(vm, XE_ERR_DEVICE, "alloc (poison)");
+  }
+  std::vector<const void*> src;
+  std::vector<void*> dst;
+  std::vector<uint64_t> words;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (!m.d_asnap[si] && dev_alloc((void**)&m.d_asnap[si], m.vals_alloc))
+      return fail(vm, XE_ERR_DEVICE, "device alloc (batch snapshot)");
+    src.push_back(m.d_vals);
+    dst.push_back(m.d_asnap[si]);
+    words.push_back(m.vals_alloc / 8);
+  }
+  XeParams P = batch_params(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, sl.d_aux);
+  P.mode = XE_MODE_PARALLEL;
+  P.poison = vm->d_poison;
+  const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+  const uint32_t grid = parallel_grid(vm, jit, general, n, P.nmaps);
+  if (general && ensure_arena(vm, false, grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+  // this batch's rollback point and zeroed records, the kernel, the replica fold, the device-side
+  // conflict decision, the records' read-back
+  if (launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), sl.d_aux, aux_used, s))
+    return fail(vm, XE_ERR_DEVICE, "prologue");
+  sl.t0.rec(s);
+  if ((jit ? launch_jit(jit, &P, grid, 256, s) : launch_interp(&P, grid, 256, s))) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+  sl.t1.rec(s);
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
+      return fail(vm, XE_ERR_DEVICE, "replica fold");
+  }
+  if (launch_epilogue(sl.d_aux, kRep, P.rep_words, P.nmaps, vm->settings.mode, vm->d_poison, s) ||
+      d2h(sl.h_aux, sl.d_aux, aux_used * 8, s))
+    return fail(vm, XE_ERR_DEVICE, "epilogue");
+  sl.done.rec(s);
+  sl.b = xe_vm::Batch{d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, s, stats};
+  sl.aux_used = aux_used;
+  sl.nmaps = P.nmaps;
+  sl.grid = grid;
+  sl.engine = jit ? XE_ENGINE_JIT : XE_ENGINE_INTERP;
+  vm->last_grid = grid;
+  vm->pending.push_back(si);
+  vm->next_slot = (si + 1) % kAsyncDepth;
+  vm->delta_base = false;
+  for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   return XE_OK;
 }
 
@@ -1685,6 +1933,7 @@ int xe_map_values_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
 int xe_map_delta(xe_vm* vm, int32_t mi, uint32_t lane, void* d_out, void* stream) {
   HostMap* m = get_map(vm, mi);
   if (!m || !d_out) return XE_ERR_INVAL;
+  if (!vm->delta_base) return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start");
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
@@ -1696,6 +1945,7 @@ int xe_map_delta(xe_vm* vm, int32_t mi, uint32_t lane, void* d_out, void* stream
 int xe_map_apply_delta(xe_vm* vm, int32_t mi, uint32_t lane, const void* d_in, void* stream) {
   HostMap* m = get_map(vm, mi);
   if (!m || !d_in) return XE_ERR_INVAL;
+  if (!vm->delta_base) return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start");
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
@@ -1714,6 +1964,7 @@ int xe_map_delta_lane(xe_vm* vm, int32_t mi, uint32_t* lane_bytes) {
 
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords) {
   if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
   const uint32_t nm = uint32_t(vm->maps.size() - 1);
   const uint32_t need = 1 + 3 * nm;
   if (nwords) *nwords = need;

@@ -90,6 +90,17 @@ def _stats_dict(s: N.BatchStats) -> dict:
             "total_ms": s.total_ms, "engine_used": s.engine_used, "grid_blocks": s.grid_blocks}
 
 
+class PendingBatch:
+    """A batch queued by VM.run_batch_device_async; owns the statistics record the library fills."""
+
+    def __init__(self, vm: "VM", st: N.BatchStats):
+        self.vm, self._st = vm, st
+
+    def stats(self) -> dict:
+        self.vm.sync()
+        return _stats_dict(self._st)
+
+
 class VM:
     def __init__(self, settings: Settings | None = None, lib: N.Lib | None = None):
         self.lib = lib or N.product()
@@ -106,11 +117,13 @@ class VM:
             raise EmulatorError(rc, "create VM")
         self.h = h
         self.map_defs: dict[int, MapDef] = {}
+        self._pending: list = []  # pipelined batches whose statistics the library still writes
 
     def close(self) -> None:
         if self.h:
             self.lib.destroy(self.h)
             self.h = None
+            self._pending.clear()
 
     def __del__(self):
         try:
@@ -264,6 +277,25 @@ class VM:
                                        d_verdicts or None, d_regs or None, stream or None, C.byref(st))
         self._check(rc, "run batch (device)")
         return _stats_dict(st)
+
+    def run_batch_device_async(self, d_umem: int, umem_len: int, d_desc: int, n: int, d_results: int = 0,
+                               d_verdicts: int = 0, d_regs: int = 0, stream: int = 0) -> "PendingBatch":
+        """Pipelined device-resident batch (xe_run_batch_device_async): queued behind the batches in
+        flight on the same stream; the result equals run_batch_device in submission order. The returned
+        handle's .stats() completes the pipeline (xe_sync) and gives this batch's statistics."""
+        st = N.BatchStats()
+        rc = self.lib.run_batch_device_async(self.h, d_umem or None, umem_len, d_desc or None, n, d_results or None,
+                                             d_verdicts or None, d_regs or None, stream or None, C.byref(st))
+        self._check(rc, "run batch (device, pipelined)")
+        pb = PendingBatch(self, st)
+        self._pending.append(pb)
+        return pb
+
+    def sync(self) -> None:
+        """Complete every pipelined batch (in-order replays included)."""
+        rc = self.lib.sync(self.h)
+        self._pending.clear()
+        self._check(rc, "sync")
 
     # ---- multi-GPU shard support
     def map_delta(self, m: int, d_out: int, stream: int = 0, lane: int = 0) -> None:

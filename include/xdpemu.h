@@ -239,6 +239,23 @@ int xe_map_push(xe_vm* vm, int32_t map_idx, const void* value);
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream,
                         xe_batch_stats* stats);
+/* Pipelined form of xe_run_batch_device for a stream of batches (a serving loop): enqueues the batch
+ * behind those still in flight on the same stream and returns without waiting. The observable result
+ * is exactly that of calling xe_run_batch_device for each batch in submission order: each batch's
+ * conflict check runs on the device at its end (an epilogue kernel); a batch that must be replayed in
+ * packet order stops the batches queued behind it from running, and xe_sync (or the next call that
+ * needs the VM's state) rolls the maps back to that batch's start and re-runs it and its successors
+ * through the synchronous path. *stats is filled when the batch completes: keep it (and the batch
+ * buffers) valid until xe_sync returns. Batches that cannot pipeline (sequential mode, ordered maps,
+ * programs that may write packet bytes) run synchronously after everything in flight. Every other
+ * entry point that reads or changes VM state completes the pipelined batches first. After pipelined
+ * batches, xe_map_delta / xe_map_apply_delta need a synchronous batch first (their base snapshot).
+ * Not a reference entry point: the Go harness runs one packet at a time. */
+int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
+                              void* d_results, void* d_verdicts, void* d_regs, void* stream,
+                              xe_batch_stats* stats);
+/* Complete every pipelined batch (replays included); returns the first error. */
+int xe_sync(xe_vm* vm);
 /* Host-memory form (end-to-end: pinned staging + hipMemcpyAsync H2D/D2H). Packet writes made by the
  * program are copied back into umem (only when the program can write packet memory at all: a
  * may-point-to analysis of the program at load). results/regs may be NULL. */

@@ -889,6 +889,9 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       m.nrep = want;
       vm->jit_idx = -1;  // the replica count is compiled into the per-program kernel
     }
+    if (xe_tuning_env("XE_PRINT_ALLOC"))  // placement experiments (tuning build only)
+      fprintf(stderr, "{\"map\": %zu, \"vals\": \"%p\", \"keys\": \"%p\", \"rep\": \"%p\", \"nrep\": %u, \"rep_stride\": %llu}\n",
+              i, (void*)m.d_vals, (void*)m.d_keys, (void*)m.d_rep, m.nrep, (unsigned long long)m.rep_stride);
   }
   std::vector<XeDevMap> dm(vm->maps.size());
   memset(dm.data(), 0, dm.size() * sizeof(XeDevMap));

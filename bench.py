@@ -283,7 +283,7 @@ def main() -> None:
 
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
-    from gobpfld_amd.shard import exchange_shards
+    from gobpfld_amd.shard import ShardEpoch
 
     name = args.config
     n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))
@@ -309,24 +309,27 @@ def main() -> None:
         return vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
                                    d_verdicts=d_ver.data_ptr(), stream=stream)
 
-    def step() -> dict:
-        st = run()
-        if world > 1:  # footprint check, then one RCCL all-reduce per map (or the in-order replay)
-            x = exchange_shards(vm, maps, dist, run, device=dev, stream=stream)
-            exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
-        return st
-
-    # one GPU: a stream of batches through the pipelined entry point (each batch's conflict check runs
-    # on the device; xe_sync completes and, if needed, replays them — all inside the timed region)
-    pipelined = world == 1 and not args.sync
+    # A stream of batches through the pipelined entry point (each batch's conflict check runs on the
+    # device; xe_sync completes and, if needed, replays them — all inside the timed region). N > 1:
+    # the batches of a call form one shard epoch, reconciled once at its end (footprint check, one
+    # RCCL all-reduce per map, or the exact in-order replay) inside the timed region.
+    pipelined = not args.sync
+    epoch = ShardEpoch(vm, maps, dist, device=dev, stream=stream) if world > 1 else None
 
     def steps(k: int) -> list[dict]:
-        if not pipelined:
-            return [step() for _ in range(k)]
-        hs = [vm.run_batch_device_async(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
-                                        d_verdicts=d_ver.data_ptr(), stream=stream) for _ in range(k)]
-        vm.sync()
-        return [h.stats() for h in hs]
+        if epoch is not None:
+            epoch.begin()
+        if pipelined:
+            hs = [vm.run_batch_device_async(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
+                                            d_verdicts=d_ver.data_ptr(), stream=stream) for _ in range(k)]
+            vm.sync()
+            sts = [h.stats() for h in hs]
+        else:
+            sts = [run() for _ in range(k)]
+        if epoch is not None:
+            x = epoch.exchange([run] * k)
+            exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
+        return sts
 
     steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -392,7 +395,7 @@ def main() -> None:
                        "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
                        "engine": sorted(engines),
                        "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps),
-                       "shard_exchanges": exchanges if world > 1 else None,
+                       "shard_exchanges": dict(exchanges, per="epoch of the timed steps") if world > 1 else None,
                        "batches": "pipelined (xe_run_batch_device_async, depth 3, device-side conflict check)"
                                   if pipelined else "synchronous (xe_run_batch_device)",
                        "grid": grid},

@@ -90,6 +90,8 @@ _SIGS = {
     "map_delta_lane": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint32)]),
     "footprint": (C.c_int, [P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
     "shard_check": (C.c_int, [P, C.c_uint32, C.c_uint32, P]),
+    "epoch_begin": (C.c_int, [P, P]),
+    "epoch_end": (C.c_int, [P]),
     "map_state_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_state_export": (C.c_int, [P, C.c_int32, P, P]),
     "map_state_import": (C.c_int, [P, C.c_int32, P, P]),
@@ -115,7 +117,8 @@ HEADER_SYMBOLS = [
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
     "xe_map_count", "xe_map_dump", "xe_map_dump_list", "xe_map_lru_order", "xe_map_push", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
     "xe_run_batch_device_async", "xe_sync", "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
-    "xe_device_count", "xe_shard_check", "xe_map_state_bytes", "xe_map_state_export", "xe_map_state_import",
+    "xe_device_count", "xe_shard_check", "xe_epoch_begin", "xe_epoch_end", "xe_map_state_bytes", "xe_map_state_export",
+    "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h

@@ -194,6 +194,29 @@ struct XeGen {
   uint32_t pad;
 };
 
+// Pipelined-batch epilogue (xe_tail_kernel, one launch after the batch's kernel): publishes the
+// batch records to host_aux (a device-visible pointer into the slot's pinned host record) and
+// zeroes them for the slot's next batch, decides on the in-order replay, and folds + snapshots the
+// ntail small maps (the next batch's rollback point, so that batch needs no prologue launch).
+#define XE_TAIL_MAPS 4
+#define XE_TAIL_MAP_WORDS 2048  // largest such value region (u64 words, 16 KB)
+struct XeTailMap {
+  unsigned long long* vals;
+  unsigned long long* rep;   // nrep replicas (nrep 0: none)
+  unsigned long long* snap;
+  uint64_t words;
+  uint64_t stride_words;
+  uint32_t nrep;
+  uint32_t pad;
+};
+struct XeTailArgs {
+  unsigned long long* aux;       // [0] flags, [16 + r * rep_words + w] wave record replica r
+  unsigned long long* host_aux;
+  uint32_t* poison;
+  uint32_t aux_words, nrep, rep_words, nmaps, mode, ntail;
+  XeTailMap tail[XE_TAIL_MAPS];
+};
+
 // per-launch parameters
 struct XeParams {
   const XeUop* prog;
@@ -233,3 +256,17 @@ struct XeParams {
 // Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in
 // packet order (same rule as the synchronous run's conflict check)
 #define XE_AUX_DECISION 1
+
+// The replay rule on the wave records OR-reduced over the replicas (orw[w] = OR of word w): an
+// ordered write or a lane out of arena, a read of a field other lanes add to, or adds of more than
+// one width on a map (xe_runtime.cpp run_conflict states it on the reduced host copy).
+template <class Words>
+XE_HD bool xe_replay_decision(uint32_t flags, Words orw, uint32_t rep_words, uint32_t nmaps, uint32_t mode) {
+  bool conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
+  for (uint32_t m = 1; m <= nmaps && m < 64 && 17 + 2 * m < rep_words; m++) {
+    if (orw[16 + 2 * m] & orw[16 + 2 * m + 1]) conflict = true;
+    const unsigned wc = unsigned(orw[XE_REC_WIDTH0 + m / 16] >> (4 * (m % 16))) & 15u;
+    if (wc & (wc - 1)) conflict = true;
+  }
+  return conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY));
+}

@@ -118,6 +118,12 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_HAS_ORDERED 1
 #endif
 
+// Paired deferral of 8-byte map adds (pend_add / pend_flush): the per-program kernel enables it when
+// a packet can make more than one such add; the interpreter keeps it on.
+#ifndef XE_PAIR_ADDS
+#define XE_PAIR_ADDS 1
+#endif
+
 // maps whose read / atomic footprints a lane keeps in registers (the rest OR straight into the wave's
 // record); a per-program kernel sets it to the VM's map count
 #ifndef XE_FP_MAPS
@@ -275,6 +281,11 @@ struct XeLane {
   uint32_t wave;            // global wave index (map value replica = wave % nrep)
   uint32_t awidth;          // atomic width classes used on maps 1..4 (4 bits per map)
   XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
+#if XE_PAIR_ADDS
+  // this packet's deferred 8-byte adds into one 16-byte block of a map value (pend_add): tag = block
+  // address | map << 48 | word mask << 56, sums of word 0 / word 1; flushed by lane_finish
+  uint64_t pb_tag, pb_s0, pb_s1;
+#endif
 };
 
 // ------------------------------------------------------------------ registers
@@ -939,12 +950,50 @@ XE_DEV void acc_apply(const XeLane& L, unsigned long long tag, unsigned long lon
   field_add(L, uint32_t((tag >> 48) & 0xffu), tag & 0xffffffffffffull, int(tag >> 56), v);
 }
 
+#if XE_PAIR_ADDS
+// Paired deferral. Memory-side atomics cost one request per 64-byte line per wave-instruction, not
+// per lane: two 8-byte adds of one packet into adjacent fields (C5's {pkts, bytes}) cost two requests
+// when the lane issues them itself, one when two neighbouring lanes issue them in the same
+// instruction (tools/calib_hash.hip: 23.5 vs 47 G adds/s). A packet's 8-byte adds that miss the
+// accumulator table therefore collect in one 16-byte block per lane, and lane_finish flushes the
+// blocks of the whole wave with word w of lane j's block on lane 2j + w. Exact: the adds commute
+// modulo 2^64 and no lane reads a field that receives adds in a parallel run (run_conflict).
+XE_DEV bool pend_add(XeLane& L, uint32_t m, uint64_t addr, uint64_t add) {
+  const uint64_t blk = (addr & ~uint64_t(15)) | (uint64_t(m) << 48);
+  const uint64_t w = (addr >> 3) & 1;
+  if (L.pb_tag && (L.pb_tag & ((1ull << 56) - 1)) != blk) return false;
+  L.pb_tag |= blk | (1ull << (56 + w));
+  if (w) L.pb_s1 += add; else L.pb_s0 += add;
+  return true;
+}
+XE_DEV void pend_word(const XeLane& L, uint64_t tag, uint64_t s, uint32_t w) {
+  if (s && ((tag >> (56 + w)) & 1)) field_add(L, uint32_t((tag >> 48) & 0xffu), (tag & 0xffffffffffffull) + 8 * w, 8, s);
+}
+// all lanes: apply every lane's block (two vector atomics for the wave) and clear it
+XE_DEV void pend_flush(XeLane& L) {
+#if defined(__HIPCC__)
+  const uint32_t lane = uint32_t(xe_lane()), w = lane & 1u;
+#pragma unroll
+  for (uint32_t h = 0; h < 2; h++) {
+    const int src = int(32 * h + (lane >> 1));
+    const uint64_t tag = __shfl(L.pb_tag, src), s0 = __shfl(L.pb_s0, src), s1 = __shfl(L.pb_s1, src);
+    pend_word(L, tag, w ? s1 : s0, w);
+  }
+#else
+  pend_word(L, L.pb_tag, L.pb_s0, 0);
+  pend_word(L, L.pb_tag, L.pb_s1, 1);
+#endif
+  L.pb_tag = L.pb_s0 = L.pb_s1 = 0;
+}
+#endif
+
 // Add `add` to the `size`-byte field at p of map m. Deferred (parallel mode): naturally aligned 4/8-
-// byte fields go through the wave's accumulator table, and 8-byte adds that reach HBM go to the
-// wave's replica. Exact in every case: the field add is modulo 2^(8*size), so adding a sum later
-// equals adding its parts now; an entry changes owner only after its sum has been taken (exchange)
-// and before any lane of this instruction adds to it (the adds re-read the tag after the claim /
-// take-over step), so no part is lost or credited to another field.
+// byte fields go through the wave's accumulator table, 8-byte adds that miss it collect in the lane's
+// paired block (pend_add) where enabled, and 8-byte adds that reach HBM go to the wave's replica.
+// Exact in every case: the field add is modulo 2^(8*size), so adding a sum later equals adding its
+// parts now; an entry changes owner only after its sum has been taken (exchange) and before any lane
+// of this instruction adds to it (the adds re-read the tag after the claim / take-over step), so no
+// part is lost or credited to another field.
 XE_DEV void wave_atomic_add_field(XeLane& L, uint32_t m, bool defer, uint8_t* p, int size, uint64_t add) {
 #if defined(XE_DEBUG_NO_ATOMIC)  // cost experiments only: map adds are dropped (results are wrong)
   return;
@@ -957,8 +1006,13 @@ XE_DEV void wave_atomic_add_field(XeLane& L, uint32_t m, bool defer, uint8_t* p,
     XE_LP(unsigned long long) tp = (XE_LP(unsigned long long))&acc->tag[k];
     XE_LP(int) sp = (XE_LP(int))&acc->score[k];
     const unsigned long long t = *tp;
+    bool pended = false;
     if (t == 0) {
       if (xe_lds_cas64(tp, 0ull, tag) == 0) *sp = 1;
+#if XE_PAIR_ADDS
+    } else if (t != tag && size == 8 && pend_add(L, m, addr, add)) {
+      pended = true;  // a miss: into this packet's paired block (the owner keeps its entry)
+#endif
     } else if (t != tag) {
       // a miss wears the owner's score down; the lane that exhausts it takes the entry over
       if (xe_lds_add32(sp, -1) <= 1 && xe_lds_cas64(tp, t, tag) == t) {
@@ -967,6 +1021,7 @@ XE_DEV void wave_atomic_add_field(XeLane& L, uint32_t m, bool defer, uint8_t* p,
         if (old) acc_apply(L, t, old);
       }
     }
+    if (pended) return;
     if (*tp == tag) {
       xe_lds_add64((XE_LP(unsigned long long))&acc->sum[k], add);
       if (t == tag) xe_lds_add32(sp, 1);
@@ -2306,6 +2361,9 @@ XE_DEV void status_from_error(int e, int& status, int& code) {
 // results, parity record, flags and batch statistics for the lane's packet (all lanes call this)
 XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, int status, int code,
                         int32_t res_pc, uint64_t steps) {
+#if XE_PAIR_ADDS
+  pend_flush(L);
+#endif
   if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
   if (status == XE_ST_INTERNAL_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
   if (valid) {
@@ -2377,6 +2435,9 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   L.wave = wave;
   L.awidth = 0;
   L.pend = pend;
+#if XE_PAIR_ADDS
+  L.pb_tag = L.pb_s0 = L.pb_s1 = 0;
+#endif
 #pragma unroll 1
   for (uint32_t k = uint32_t(xe_lane()); k < XE_ACC; k += XE_WAVE) { pend->tag[k] = 0; pend->sum[k] = 0; pend->score[k] = 0; }
 #pragma unroll
@@ -2473,3 +2534,4 @@ XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
     }
   }
 }
+

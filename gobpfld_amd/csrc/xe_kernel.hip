@@ -84,42 +84,57 @@ extern "C" __global__ void xe_prologue_kernel(XeProlog A) {
     for (uint64_t i = tid; i < A.words[g]; i += nth) A.dst[g][i] = A.src[g][i];
 }
 
-// Pipelined-batch epilogue (xe_run_batch_device_async): the synchronous run's conflict rule evaluated
-// on the device, so the next batch, already queued behind this one, knows before it starts whether
-// this batch will be replayed in order. One block: thread w ORs word w of the per-wave records over
-// the replicas, thread 0 decides; a replay sets the poison word (the next launches do nothing) and
-// aux[XE_AUX_DECISION]. Layout of aux: xe_runtime.cpp (read_aux / reduce).
-extern "C" __global__ void __launch_bounds__(256) xe_epilogue_kernel(unsigned long long* aux, uint32_t nrep, uint32_t rep_words,
-                                                                     uint32_t nmaps, uint32_t mode, uint32_t* poison) {
-  __shared__ unsigned long long orw[256];
-  const uint32_t t = threadIdx.x;
-  unsigned long long o = 0;
-  if (t < rep_words)
-    for (uint32_t r = 0; r < nrep; r++) o |= aux[16 + uint64_t(r) * rep_words + t];
-  orw[t] = o;
+// Pipelined-batch epilogue (XeTailArgs, xe_internal.h): one block after the batch's kernel. A launch
+// boundary orders it after every wave of the batch, so plain loads see all their adds and records.
+// Thread w ORs record word w over the replicas (LDS), thread 0 decides the replay exactly as the
+// synchronous run does; then the small maps are folded and snapshotted for the next batch unless an
+// earlier batch is being replayed (poison set): that replay restarts from its own snapshot, which
+// this slot's successor may hold (the ring wraps), and every later batch re-runs synchronously.
+extern "C" __global__ void __launch_bounds__(1024) xe_tail_kernel(XeTailArgs A) {
+  __shared__ unsigned long long orw[257];
+  const uint32_t t = threadIdx.x, nt = blockDim.x;
+  for (uint32_t w = t; w <= 256; w += nt) orw[w] = 0;
+  const bool poisoned = *(volatile uint32_t*)A.poison != 0;
   __syncthreads();
-  if (t != 0) return;
-  if (*poison) return;  // this batch did not run: an earlier one is being replayed
-  const uint32_t flags = uint32_t(aux[0]);
-  bool conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
-  for (uint32_t m = 1; m <= nmaps && m < 64 && 17 + 2 * m < 256; m++) {
-    if (orw[16 + 2 * m] & orw[16 + 2 * m + 1]) conflict = true;
-    const unsigned wc = unsigned(orw[XE_REC_WIDTH0 + m / 16] >> (4 * (m % 16))) & 15u;
-    if (wc & (wc - 1)) conflict = true;
+  for (uint32_t i = t; i < A.aux_words; i += nt) {
+    const unsigned long long v = A.aux[i];
+    if (v) A.aux[i] = 0;
+    A.host_aux[i] = v;
+    if (i == 0) orw[256] = v;
+    else if (i >= 16 && v) atomicOr(&orw[(i - 16) % A.rep_words], v);
   }
-  const bool replay = conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY));
-  aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
-  if (replay) *poison = 1u;
+  __syncthreads();
+  if (t == 0) {
+    const bool replay = !poisoned && xe_replay_decision(uint32_t(orw[256]), orw, A.rep_words, A.nmaps, A.mode);
+    A.host_aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
+    if (replay) *A.poison = 1u;
+  }
+  if (poisoned) return;
+  for (uint32_t f = 0; f < A.ntail; f++) {
+    const XeTailMap& T = A.tail[f];
+    for (uint64_t i = t; i < T.words; i += nt) {
+      unsigned long long r[16];
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++) r[k] = k < T.nrep ? T.rep[k * T.stride_words + i] : 0ull;
+      unsigned long long s = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++) {
+        s += r[k];
+        if (r[k]) T.rep[k * T.stride_words + i] = 0;
+      }
+      const unsigned long long v = T.vals[i] + s;
+      if (s) T.vals[i] = v;
+      T.snap[i] = v;
+    }
+  }
+}
+extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s) {
+  if (A->rep_words > 256) return -1;
+  hipLaunchKernelGGL(xe_tail_kernel, dim3(1), dim3(1024), 0, s, *A);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // host-side launchers (called from xe_runtime.cpp)
-extern "C" int xe_launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison,
-                                  hipStream_t s) {
-  if (rep_words > 256) return -1;
-  hipLaunchKernelGGL(xe_epilogue_kernel, dim3(1), dim3(256), 0, s, (unsigned long long*)aux, nrep, rep_words, nmaps, mode,
-                     (uint32_t*)poison);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
   hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -33,8 +33,7 @@ extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, 
 extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
-extern "C" int xe_launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison,
-                                  hipStream_t s);
+extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
                             bool* general, const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -111,7 +110,7 @@ int launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, x
 }
 int launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg, void* zero, uint64_t zw,
                     xe_stream_t) {
-  memset(zero, 0, zw * 8);
+  if (zw) memset(zero, 0, zw * 8);
   for (uint32_t g = 0; g < nseg; g++) memcpy(dst[g], src[g], words[g] * 8);
   return 0;
 }
@@ -122,26 +121,34 @@ int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t 
     for (uint32_t k = 0; k < nrep; k++) { v[i] += r[k * sw + i]; r[k * sw + i] = 0; }
   return 0;
 }
-int launch_epilogue(void* auxp, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison, xe_stream_t) {
-  unsigned long long* aux = (unsigned long long*)auxp;
-  std::vector<unsigned long long> orw(rep_words, 0);
-  for (uint32_t t = 0; t < rep_words; t++)
-    for (uint32_t r = 0; r < nrep; r++) orw[t] |= aux[16 + uint64_t(r) * rep_words + t];
-  if (*(uint32_t*)poison) return 0;
-  const uint32_t flags = uint32_t(aux[0]);
-  bool conflict = (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) != 0;
-  for (uint32_t m = 1; m <= nmaps && m < 64; m++) {
-    if (orw[16 + 2 * m] & orw[16 + 2 * m + 1]) conflict = true;
-    const unsigned wc = unsigned(orw[XE_REC_WIDTH0 + m / 16] >> (4 * (m % 16))) & 15u;
-    if (wc & (wc - 1)) conflict = true;
+int launch_tail(const XeTailArgs* A, xe_stream_t) {  // xe_kernel.hip xe_tail_kernel, one thread
+  unsigned long long orw[257] = {};
+  const bool poisoned = *A->poison != 0;
+  for (uint32_t i = 0; i < A->aux_words; i++) {
+    const unsigned long long v = A->aux[i];
+    A->aux[i] = 0;
+    A->host_aux[i] = v;
+    if (i == 0) orw[256] = v;
+    else if (i >= 16) orw[(i - 16) % A->rep_words] |= v;
   }
-  const bool replay = conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY));
-  aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
-  if (replay) *(uint32_t*)poison = 1u;
+  const bool replay = !poisoned && xe_replay_decision(uint32_t(orw[256]), orw, A->rep_words, A->nmaps, A->mode);
+  A->host_aux[XE_AUX_DECISION] = replay ? 1ull : 0ull;
+  if (replay) *A->poison = 1u;
+  if (poisoned) return 0;
+  for (uint32_t f = 0; f < A->ntail; f++) {
+    const XeTailMap& T = A->tail[f];
+    for (uint64_t i = 0; i < T.words; i++) {
+      unsigned long long s = 0;
+      for (uint32_t k = 0; k < T.nrep; k++) { s += T.rep[k * T.stride_words + i]; T.rep[k * T.stride_words + i] = 0; }
+      T.vals[i] += s;
+      T.snap[i] = T.vals[i];
+    }
+  }
   return 0;
 }
 int host_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
 void host_free(void* p) { free(p); }
+int host_device_ptr(void** d, void* h) { *d = h; return 0; }
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
@@ -177,11 +184,11 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
                     xe_stream_t s) {
   return xe_launch_prologue(src, dst, words, nseg, zero, zw, s);
 }
-int launch_epilogue(void* aux, uint32_t nrep, uint32_t rep_words, uint32_t nmaps, uint32_t mode, void* poison, xe_stream_t s) {
-  return xe_launch_epilogue(aux, nrep, rep_words, nmaps, mode, poison, s);
-}
 int host_alloc(void** p, size_t n) { return hipHostMalloc(p, n ? n : 8, hipHostMallocDefault) == hipSuccess ? 0 : -1; }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
+int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
+// device-visible address of pinned host memory (hipHostMalloc default: mapped, coherent)
+int host_device_ptr(void** d, void* h) { return hipHostGetDevicePointer(d, h, 0) == hipSuccess ? 0 : -1; }
 struct Timer {
   hipEvent_t e = nullptr;
   void init() { if (!e) (void)hipEventCreate(&e); }
@@ -431,6 +438,8 @@ struct HostMap {
   uint64_t rep_stride = 0;
   uint32_t lane = 0;    // width of the map adds of the last run (delta lanes): 0 none, 8 when mixed
   uint32_t wclass = 0;  // width classes of the last run's adds (bit 0: 1 B ... bit 3: 8 B)
+  uint32_t ewclass = 0; // width classes of the adds since xe_epoch_begin
+  uint8_t* d_ebase = nullptr;  // values at xe_epoch_begin (the epoch's delta base)
   uint32_t live = 0;    // HASH: entry count for replica sizing (host count, refreshed after ordered runs)
   bool host_dirty = true, dev_dirty = false;
   // ordered maps (LRU_HASH / QUEUE / STACK / PERF_EVENT_ARRAY): the host mirror in Go order —
@@ -556,15 +565,16 @@ struct xe_vm {
   uint64_t ord_slack = 4096, ord_slack_bytes = 1 << 20;
   // pipelined batches (xe_run_batch_device_async): a ring of slots, each with its own statistics /
   // footprint buffer (device + pinned host copy), events and map rollback points; `pending` holds the
-  // slots in flight in submission order. d_poison: set by an epilogue whose batch must be replayed.
+  // slots in flight in submission order. d_poison: set by a batch epilogue whose batch must be replayed.
   struct Batch {
     void* d_umem = nullptr; uint64_t umem_len = 0; const void* d_desc = nullptr; uint32_t n = 0;
     void* d_results = nullptr; void* d_verdicts = nullptr; void* d_regs = nullptr;
     xe_stream_t s = nullptr; xe_batch_stats* stats = nullptr;
   };
   struct Slot {
-    unsigned long long* d_aux = nullptr;
+    unsigned long long* d_aux = nullptr;    // zero whenever no batch of the slot is running
     unsigned long long* h_aux = nullptr;
+    unsigned long long* h_aux_dev = nullptr;  // h_aux as the batch epilogue writes it
     Timer t0, t1, done;
     Batch b;
     size_t aux_used = 0;
@@ -574,8 +584,17 @@ struct xe_vm {
   std::vector<uint32_t> pending;
   uint32_t next_slot = 0;
   uint32_t* d_poison = nullptr;
+  // slot whose small-map snapshots the last pipelined batch's tail wrote (-1: none valid); anything
+  // else that writes device map values invalidates it (stage_invalidate)
+  int32_t staged_slot = -1;
   bool draining = false;
   bool delta_base = true;  // the map snapshots are the start of the last batch (false after async batches)
+  // shard epoch (xe_epoch_begin): every run since then ORs its footprint here, and the map deltas are
+  // taken against the values at the epoch's start (HostMap::d_ebase)
+  bool epoch_open = false;
+  std::vector<unsigned long long> epoch_fp;
+  uint32_t epoch_flags = 0;
+  bool epoch_seq = false;
 };
 
 namespace {
@@ -583,6 +602,7 @@ namespace {
 constexpr uint32_t kRep = 64;                  // statistics / footprint replicas
 constexpr uint32_t kRepWords = 16 + 2 * 64;      // per replica: stats + (read, atomic) per map
 constexpr size_t kAuxWords = 16 + size_t(kRep) * kRepWords;
+constexpr uint64_t kTailMapBytes = 8 * XE_TAIL_MAP_WORDS;  // value regions the batch epilogue folds / snapshots
 
 int fail(xe_vm* vm, int rc, const std::string& msg) {
   if (vm) vm->last_error = msg;
@@ -603,13 +623,15 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 // counter's atomics, bounded in memory (HBM is plentiful, but every run folds all replicas).
 // Replicas of a value region spread contended map adds over nrep copies (wave % nrep), folded into
 // the region after the run. Chosen per run from the live bytes (ARRAY: the region; HASH: entries x
-// value size), bounded so the fold reads at most 128 MB. Measured: C3 (64K Zipf-hot flows in a
-// 1M-entry table) needs >= 4 (1 replica: 8.2 ms, 2: 1.1-4.0 ms depending on placement, 4: 1.08 ms);
-// C5 (1M uniform flows) is fastest with none (3.45 ms; each doubling costs ~5 %).
+// value size), bounded so the fold reads at most ~160 MB. Measured: C3 (64K Zipf-hot flows in a
+// 1M-entry table, a 32 MB + 16 B value region) needs >= 4 (1 replica: 8.2 ms, 2: 1.1-4.0 ms from run
+// to run, 4: 1.08 ms, 16: 1.05-1.09 ms over 6 VM placements); C5 (1M uniform flows) is fastest with
+// none (3.45 ms; each doubling costs ~5 %). The bound once sat at exactly 128 MB, which the region's
+// extra empty-key slot pushed C3 past (2 replicas, the bimodal case).
 uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc) {
   if (const char* e = xe_tuning_env("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));
   uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
-  while (want > 1 && uint64_t(want) * vals_alloc > (128ull << 20)) want >>= 1;
+  while (want > 1 && uint64_t(want) * vals_alloc > (160ull << 20)) want >>= 1;
   return want;
 }
 
@@ -629,6 +651,8 @@ int map_alloc_device(HostMap& m) {
 
 void map_free_device(HostMap& m) {
   for (auto& p : m.d_asnap) { dev_free(p); p = nullptr; }
+  dev_free(m.d_ebase);
+  m.d_ebase = nullptr;
   dev_free(m.d_vals); dev_free(m.d_snap); dev_free(m.d_keys); dev_free(m.d_state); dev_free(m.d_count); dev_free(m.d_rep);
   m.d_vals = m.d_snap = nullptr; m.d_keys = nullptr; m.d_state = m.d_count = nullptr; m.d_rep = nullptr;
   dev_free(m.d_hdr); dev_free(m.d_link); dev_free(m.d_elen); dev_free(m.d_rec);
@@ -876,7 +900,10 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
   vm->d_prog_len = vm->programs[vm->entry].size();
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
-    if (m.host_dirty && map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+    if (m.host_dirty) {
+      vm->staged_slot = -1;  // the device values change under the staged snapshots
+      if (map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
+    }
     const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
     const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc) : 1u;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
@@ -1062,6 +1089,7 @@ int xe_set_entrypoint(xe_vm* vm, int32_t idx) {  // emulator/vm.go:100-108
 
 int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_len, int32_t* idx) {
   if (!vm || !def) return XE_ERR_INVAL;
+  vm->staged_slot = -1;
   if (int rc = xe_sync(vm)) return rc;
   if (vm->maps.size() > XE_H_MAX_MAPS) return fail(vm, XE_ERR_UNSUPPORTED, "at most 63 maps");
   HostMap m;
@@ -1531,12 +1559,27 @@ bool run_conflict(const std::vector<unsigned long long>& red, uint32_t nmaps) {
 }
 
 // per-map add widths of the last run (the lanes of the cross-shard deltas)
+uint32_t lane_of(unsigned wc) { return wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u; }
+
 void record_widths(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t nmaps) {
   for (uint32_t m = 1; m <= nmaps && m < 64; m++) {
     const unsigned wc = unsigned(red[XE_REC_WIDTH0 + 2 + m / 16] >> (4 * (m % 16))) & 15u;
     vm->maps[m].wclass = wc;
-    vm->maps[m].lane = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
+    vm->maps[m].lane = lane_of(wc);
+    vm->maps[m].ewclass |= wc;
   }
+}
+
+// the last run's flags, mode and footprint (xe_footprint), ORed into the open shard epoch
+void note_run(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t mode) {
+  vm->last_flags = uint32_t(red[0]);
+  vm->last_mode = mode;
+  vm->last_fp.assign(red.begin() + 16, red.end());
+  if (!vm->epoch_open) return;
+  vm->epoch_flags |= vm->last_flags;
+  vm->epoch_seq = vm->epoch_seq || mode == XE_MODE_SEQUENTIAL;
+  if (vm->epoch_fp.size() < vm->last_fp.size()) vm->epoch_fp.resize(vm->last_fp.size(), 0);
+  for (size_t i = 0; i < vm->last_fp.size(); i++) vm->epoch_fp[i] |= vm->last_fp[i];
 }
 
 }  // namespace
@@ -1544,6 +1587,7 @@ void record_widths(xe_vm* vm, const std::vector<unsigned long long>& red, uint32
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
+  vm->staged_slot = -1;  // this run writes the maps outside the pipeline
   if (stats) memset(stats, 0, sizeof *stats);
   if (int rc = xe_sync(vm)) return rc;  // pipelined batches first: they precede this one
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
@@ -1690,9 +1734,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (size_t i = 1; i < vm->maps.size(); i++)
       if (vm->maps[i].dkind == XE_DM_HASH) vm->maps[i].live = counts[i];
   }
-  vm->last_flags = uint32_t(red[0]);
-  vm->last_mode = used;
-  vm->last_fp.assign(red.begin() + 16, red.end());
+  note_run(vm, red, used);
   for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   if (stats) {
     stats->packets = n;
@@ -1722,6 +1764,7 @@ int complete_oldest(xe_vm* vm) {
   }
   const unsigned long long* aux = sl.h_aux;
   if (aux[XE_AUX_DECISION]) {
+    vm->staged_slot = -1;
     const xe_stream_t s = sl.b.s;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
@@ -1740,9 +1783,7 @@ int complete_oldest(xe_vm* vm) {
   std::vector<unsigned long long> red;
   reduce_aux(aux, sl.nmaps, 16 + 2 * (sl.nmaps + 1), red);
   record_widths(vm, red, sl.nmaps);
-  vm->last_flags = uint32_t(red[0]);
-  vm->last_mode = XE_MODE_PARALLEL;
-  vm->last_fp.assign(red.begin() + 16, red.end());
+  note_run(vm, red, XE_MODE_PARALLEL);
   if (xe_batch_stats* st = sl.b.stats) {
     st->packets = sl.b.n;
     st->steps = red[1];
@@ -1795,46 +1836,79 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   if (int rc = select_engine(vm, jit, jit_general)) return rc;
   const bool general = !jit || jit_general;
 
-  const uint32_t si = vm->next_slot;
+  const uint32_t si = vm->next_slot, nsi = (si + 1) % kAsyncDepth;
   xe_vm::Slot& sl = vm->slots[si];
-  if ((!sl.d_aux && dev_alloc((void**)&sl.d_aux, kAuxWords * 8)) || (!sl.h_aux && host_alloc((void**)&sl.h_aux, kAuxWords * 8)))
-    return fail(vm, XE_ERR_DEVICE, "alloc (pipelined batch records)");
+  if (!sl.d_aux) {  // the slot's records start zeroed; every batch epilogue zeroes them again
+    if (dev_alloc((void**)&sl.d_aux, kAuxWords * 8) || dmemset(sl.d_aux, 0, kAuxWords * 8, s))
+      return fail(vm, XE_ERR_DEVICE, "alloc (pipelined batch records)");
+  }
+  if (!sl.h_aux) {
+    if (host_alloc((void**)&sl.h_aux, kAuxWords * 8) || host_device_ptr((void**)&sl.h_aux_dev, sl.h_aux))
+      return fail(vm, XE_ERR_DEVICE, "alloc (pipelined batch records)");
+  }
   if (!vm->d_poison) {
     if (dev_alloc((void**)&vm->d_poison, 8) || dmemset(vm->d_poison, 0, 8, s)) return fail(vm, XE_ERR_DEVICE, "alloc (poison)");
-  }
-  std::vector<const void*> src;
-  std::vector<void*> dst;
-  std::vector<uint64_t> words;
-  for (size_t i = 1; i < vm->maps.size(); i++) {
-    HostMap& m = vm->maps[i];
-    if (!m.d_asnap[si] && dev_alloc((void**)&m.d_asnap[si], m.vals_alloc))
-      return fail(vm, XE_ERR_DEVICE, "device alloc (batch snapshot)");
-    src.push_back(m.d_vals);
-    dst.push_back(m.d_asnap[si]);
-    words.push_back(m.vals_alloc / 8);
   }
   XeParams P = batch_params(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, sl.d_aux);
   P.mode = XE_MODE_PARALLEL;
   P.poison = vm->d_poison;
   const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+  // One epilogue launch publishes the records to the pinned host copy and decides on the replay;
+  // small maps are folded and snapshotted for the next batch there too, the others keep the
+  // prologue snapshot and their own fold launch. This batch's rollback point: the snapshot the
+  // previous batch's epilogue staged, when nothing has written the maps since.
+  const bool staged = vm->staged_slot == int32_t(si) && !vm->pending.empty() && vm->slots[vm->pending.back()].b.s == s;
+  XeTailArgs A{};
+  A.aux = sl.d_aux;
+  A.host_aux = sl.h_aux_dev;
+  A.poison = vm->d_poison;
+  A.aux_words = uint32_t(aux_used);
+  A.nrep = kRep;
+  A.rep_words = P.rep_words;
+  A.nmaps = P.nmaps;
+  A.mode = vm->settings.mode;
+  std::vector<const void*> src;
+  std::vector<void*> dst;
+  std::vector<uint64_t> words;
+  std::vector<size_t> big;  // maps folded by their own launch
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    for (uint32_t k : {si, nsi})
+      if (!m.d_asnap[k] && dev_alloc((void**)&m.d_asnap[k], m.vals_alloc))
+        return fail(vm, XE_ERR_DEVICE, "device alloc (batch snapshot)");
+    const bool small = m.vals_alloc <= kTailMapBytes && A.ntail < XE_TAIL_MAPS;
+    if (small) {
+      XeTailMap& T = A.tail[A.ntail++];
+      T.vals = (unsigned long long*)m.d_vals;
+      T.rep = (unsigned long long*)m.d_rep;
+      T.snap = (unsigned long long*)m.d_asnap[nsi];
+      T.words = m.vals_alloc / 8;
+      T.stride_words = m.rep_stride / 8;
+      T.nrep = m.nrep > 1 ? m.nrep : 0;
+    } else {
+      big.push_back(i);
+    }
+    if (!small || !staged) {
+      src.push_back(m.d_vals);
+      dst.push_back(m.d_asnap[si]);
+      words.push_back(m.vals_alloc / 8);
+    }
+  }
   const uint32_t grid = parallel_grid(vm, jit, general, n, P.nmaps);
   if (general && ensure_arena(vm, false, grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
-  // this batch's rollback point and zeroed records, the kernel, the replica fold, the device-side
-  // conflict decision, the records' read-back
-  if (launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), sl.d_aux, aux_used, s))
+  if (!src.empty() && launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), nullptr, 0, s))
     return fail(vm, XE_ERR_DEVICE, "prologue");
   sl.t0.rec(s);
   if ((jit ? launch_jit(jit, &P, grid, 256, s) : launch_interp(&P, grid, 256, s))) return fail(vm, XE_ERR_DEVICE, "kernel launch");
   sl.t1.rec(s);
-  for (size_t i = 1; i < vm->maps.size(); i++) {
+  for (size_t i : big) {
     HostMap& m = vm->maps[i];
     if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
       return fail(vm, XE_ERR_DEVICE, "replica fold");
   }
-  if (launch_epilogue(sl.d_aux, kRep, P.rep_words, P.nmaps, vm->settings.mode, vm->d_poison, s) ||
-      d2h(sl.h_aux, sl.d_aux, aux_used * 8, s))
-    return fail(vm, XE_ERR_DEVICE, "epilogue");
+  if (launch_tail(&A, s)) return fail(vm, XE_ERR_DEVICE, "epilogue");
   sl.done.rec(s);
+  vm->staged_slot = int32_t(nsi);
   sl.b = xe_vm::Batch{d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, s, stats};
   sl.aux_used = aux_used;
   sl.nmaps = P.nmaps;
@@ -1936,32 +2010,79 @@ int xe_map_values_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
 int xe_map_delta(xe_vm* vm, int32_t mi, uint32_t lane, void* d_out, void* stream) {
   HostMap* m = get_map(vm, mi);
   if (!m || !d_out) return XE_ERR_INVAL;
-  if (!vm->delta_base) return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start");
+  if (!vm->epoch_open && !vm->delta_base)
+    return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start or a shard epoch");
+  if (vm->epoch_open)
+    if (int rc = xe_sync(vm)) return rc;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
-  if (launch_delta(m->d_vals, m->d_snap, d_out, m->vals_alloc, lane ? lane : m->lane ? m->lane : 8, s) || dsync(s))
+  const uint32_t dl = vm->epoch_open ? lane_of(m->ewclass) : m->lane;
+  if (launch_delta(m->d_vals, vm->epoch_open ? m->d_ebase : m->d_snap, d_out, m->vals_alloc, lane ? lane : dl ? dl : 8, s) ||
+      dsync(s))
     return fail(vm, XE_ERR_DEVICE, "delta");
   return XE_OK;
 }
 
 int xe_map_apply_delta(xe_vm* vm, int32_t mi, uint32_t lane, const void* d_in, void* stream) {
+  if (vm) vm->staged_slot = -1;
   HostMap* m = get_map(vm, mi);
   if (!m || !d_in) return XE_ERR_INVAL;
-  if (!vm->delta_base) return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start");
+  if (!vm->epoch_open && !vm->delta_base)
+    return fail(vm, XE_ERR_INVAL, "map deltas are taken against a synchronous batch's start or a shard epoch");
+  if (vm->epoch_open)
+    if (int rc = xe_sync(vm)) return rc;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   if (lane != 0 && lane != 1 && lane != 2 && lane != 4 && lane != 8) return XE_ERR_INVAL;
-  if (launch_apply_delta(m->d_vals, m->d_snap, d_in, m->vals_alloc, lane ? lane : m->lane ? m->lane : 8, s) || dsync(s))
+  const uint32_t dl = vm->epoch_open ? lane_of(m->ewclass) : m->lane;
+  if (launch_apply_delta(m->d_vals, vm->epoch_open ? m->d_ebase : m->d_snap, d_in, m->vals_alloc, lane ? lane : dl ? dl : 8, s) ||
+      dsync(s))
     return fail(vm, XE_ERR_DEVICE, "apply delta");
   m->dev_dirty = true;
+  return XE_OK;
+}
+
+// Shard epochs: deltas over several batches (synchronous or pipelined) against the values at the
+// epoch's start, with the footprints of every batch in between ORed together.
+int xe_epoch_begin(xe_vm* vm, void* stream) {
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  if (set_device(vm->settings.device)) return fail(vm, XE_ERR_DEVICE, "hipSetDevice failed");
+  xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (int rc = prepare_run(vm, s)) return rc;  // host-side map changes reach the device first
+  std::vector<const void*> src;
+  std::vector<void*> dst;
+  std::vector<uint64_t> words;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    m.ewclass = 0;
+    if (m.ordered()) continue;
+    if (!m.d_ebase && dev_alloc((void**)&m.d_ebase, m.vals_alloc)) return fail(vm, XE_ERR_NOMEM, "device alloc (epoch base)");
+    src.push_back(m.d_vals);
+    dst.push_back(m.d_ebase);
+    words.push_back(m.vals_alloc / 8);
+  }
+  if (!src.empty() && (launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), nullptr, 0, s) || dsync(s)))
+    return fail(vm, XE_ERR_DEVICE, "epoch snapshot");
+  vm->epoch_open = true;
+  vm->epoch_fp.assign(16 + 2 * (vm->maps.size() + 1), 0);
+  vm->epoch_flags = 0;
+  vm->epoch_seq = false;
+  return XE_OK;
+}
+
+int xe_epoch_end(xe_vm* vm) {
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  vm->epoch_open = false;
   return XE_OK;
 }
 
 int xe_map_delta_lane(xe_vm* vm, int32_t mi, uint32_t* lane_bytes) {
   HostMap* m = get_map(vm, mi);
   if (!m || !lane_bytes) return XE_ERR_INVAL;
-  *lane_bytes = m->lane;
+  *lane_bytes = vm->epoch_open ? lane_of(m->ewclass) : m->lane;
   return XE_OK;
 }
 
@@ -1973,16 +2094,19 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
   if (nwords) *nwords = need;
   if (!out) return XE_OK;
   if (cap_words < need) return XE_ERR_INVAL;
-  uint64_t f = 0;
-  if (vm->last_flags & XE_FLAG_ORDERED) f |= XE_FPF_ORDERED;
-  if (vm->last_mode == XE_MODE_SEQUENTIAL) f |= XE_FPF_SEQUENTIAL;
-  if (vm->last_flags & XE_FLAG_UNALIGNED) f |= XE_FPF_UNALIGNED;
+  const bool ep = vm->epoch_open;
+  const uint32_t flags = ep ? vm->epoch_flags : vm->last_flags;
+  const std::vector<unsigned long long>& fp = ep ? vm->epoch_fp : vm->last_fp;
+  uint64_t f = ep ? XE_FPF_EPOCH : 0;
+  if (flags & XE_FLAG_ORDERED) f |= XE_FPF_ORDERED;
+  if (ep ? vm->epoch_seq : vm->last_mode == XE_MODE_SEQUENTIAL) f |= XE_FPF_SEQUENTIAL;
+  if (flags & XE_FLAG_UNALIGNED) f |= XE_FPF_UNALIGNED;
   out[0] = f;
   for (uint32_t m = 1; m <= nm; m++) {
     const size_t r = 2 * size_t(m);
-    out[1 + 3 * (m - 1)] = r < vm->last_fp.size() ? vm->last_fp[r] : 0;
-    out[2 + 3 * (m - 1)] = r + 1 < vm->last_fp.size() ? vm->last_fp[r + 1] : 0;
-    out[3 + 3 * (m - 1)] = vm->maps[m].wclass;
+    out[1 + 3 * (m - 1)] = r < fp.size() ? fp[r] : 0;
+    out[2 + 3 * (m - 1)] = r + 1 < fp.size() ? fp[r + 1] : 0;
+    out[3 + 3 * (m - 1)] = ep ? vm->maps[m].ewclass : vm->maps[m].wclass;
   }
   return XE_OK;
 }
@@ -1990,7 +2114,8 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
 int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_t* lanes) {
   if (!fps || !ngpus || nwords < 1 || (nwords - 1) % 3) return XE_ERR_INVAL;
   const uint32_t nm = (nwords - 1) / 3;
-  bool ok = true;
+  bool ok = true, epoch = false;
+  for (uint32_t k = 0; k < ngpus; k++) epoch = epoch || (fps[size_t(k) * nwords] & XE_FPF_EPOCH);
   for (uint32_t m = 0; m < nm; m++) {
     uint64_t added = 0;  // fields earlier shards added to
     uint32_t wc = 0;
@@ -1999,6 +2124,15 @@ int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_
       if (f[1 + 3 * m] & added) ok = false;  // shard k read a field an earlier shard changed
       added |= f[2 + 3 * m];
       wc |= uint32_t(f[3 + 3 * m]);
+    }
+    // An epoch spans several batches: a shard's reads in a later batch follow every shard's adds of
+    // the earlier ones in the reference's order (batch after batch, shards in order), so a read may
+    // meet no other shard's adds at all.
+    for (uint32_t k = 0; epoch && k < ngpus; k++) {
+      uint64_t others = 0;
+      for (uint32_t j = 0; j < ngpus; j++)
+        if (j != k) others |= fps[size_t(j) * nwords + 2 + 3 * m];
+      if (fps[size_t(k) * nwords + 1 + 3 * m] & others) ok = false;
     }
     if (wc & (wc - 1)) ok = false;  // two widths: a narrow add's carry stops at its own field
     if (lanes) lanes[m] = wc == 0u ? 0u : wc == 1u ? 1u : wc == 2u ? 2u : wc == 4u ? 4u : 8u;
@@ -2034,6 +2168,7 @@ int xe_map_state_export(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
 }
 
 int xe_map_state_import(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
+  if (vm) vm->staged_slot = -1;
   HostMap* m = get_map(vm, mi);
   if (!m || !d_in) return XE_ERR_INVAL;
   set_device(vm->settings.device);

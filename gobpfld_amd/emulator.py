@@ -310,8 +310,15 @@ class VM:
     def map_apply_delta(self, m: int, d_in: int, stream: int = 0, lane: int = 0) -> None:
         self._check(self.lib.map_apply_delta(self.h, m, lane, d_in, stream or None), "map apply delta")
 
+    def epoch_begin(self, stream: int = 0) -> None:
+        """xe_epoch_begin: later map deltas / footprints cover every batch from here (a shard epoch)."""
+        self._check(self.lib.epoch_begin(self.h, stream or None), "epoch begin")
+
+    def epoch_end(self) -> None:
+        self._check(self.lib.epoch_end(self.h), "epoch end")
+
     def footprint(self) -> np.ndarray:
-        """xe_footprint record of the last run: [flags, (read, add, widths) per map]."""
+        """xe_footprint record of the last run (or of the open shard epoch): [flags, (read, add, widths) per map]."""
         nw = C.c_uint32()
         self._check(self.lib.footprint(self.h, None, 0, C.byref(nw)), "footprint")
         out = np.zeros(nw.value, dtype=np.uint64)

@@ -288,6 +288,7 @@ int xe_map_delta_lane(xe_vm* vm, int32_t map_idx, uint32_t* lane_bytes);
 #define XE_FPF_ORDERED 1    /* a lane needed a non-commutative map write */
 #define XE_FPF_SEQUENTIAL 2 /* the results come from the exact ordered replay (map writes in order) */
 #define XE_FPF_UNALIGNED 4  /* a map add was not aligned to its own width */
+#define XE_FPF_EPOCH 8      /* the record covers a shard epoch (xe_epoch_begin): several batches */
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords);
 /* Cross-shard exactness check over the footprints (xe_footprint records, nwords each) of ngpus
  * shards given in shard order. Returns 1 when init + the sum of the per-map deltas equals the state
@@ -296,6 +297,16 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
  * width per map everywhere, aligned adds. lanes[m - 1] receives the lane of map m (0 = no adds).
  * Returns 0 when the shards must be replayed in order instead. */
 int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_t* lanes);
+/* Shard epoch: from xe_epoch_begin (after the batches before it are complete) until xe_epoch_end,
+ * xe_footprint ORs the footprints of every batch run in between (synchronous and pipelined, flag
+ * XE_FPF_EPOCH) and xe_map_delta / xe_map_apply_delta / xe_map_delta_lane work against the map values
+ * at the epoch's start, so shards can run many batches and exchange once. With XE_FPF_EPOCH
+ * xe_shard_check also refuses a read of a field ANY other shard added to (a later batch of one shard
+ * follows every shard's earlier batches in the reference's order). Replaces the per-batch exchange
+ * of SURVEY §8e for streams of batches; the reference is one VM walking every packet in order
+ * (emulator/vm.go:110-173 per packet). */
+int xe_epoch_begin(xe_vm* vm, void* stream);
+int xe_epoch_end(xe_vm* vm);
 /* Whole map state (values, hash slot records and entry count) as a device byte image, for the in-order
  * shard replay: export on the shard that finished, import on the next (same map geometry). */
 int xe_map_state_bytes(xe_vm* vm, int32_t map_idx, uint64_t* bytes);

@@ -48,9 +48,9 @@ def batches(n_batches: int, n: int, marked: set[int]):
     return out
 
 
-def oracle_stream(oracle_lib, prog, bs):
+def oracle_stream(oracle_lib, prog, bs, entries=8):
     vm = VM(Settings(), lib=oracle_lib)
-    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, 8))
+    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, entries))
     vm.set_entrypoint(vm.add_raw_program(prog))
     ver = [vm.run_batch(u.copy(), d, want_regs=False).verdicts for u, d in bs]
     dump = vm.map_dump(m)
@@ -58,10 +58,10 @@ def oracle_stream(oracle_lib, prog, bs):
     return ver, dump
 
 
-def host_stream(lib, prog, bs, use_async: bool, mode=0):
+def host_stream(lib, prog, bs, use_async: bool, mode=0, entries=8):
     """Run the batches through the device-resident entry points of the host simulation (host memory)."""
     vm = VM(Settings(mode=mode), lib=lib)
-    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, 8))
+    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, entries))
     vm.set_entrypoint(vm.add_raw_program(prog))
     keep, handles = [], []
     for u, d in bs:
@@ -76,13 +76,16 @@ def host_stream(lib, prog, bs, use_async: bool, mode=0):
     return [k[2] for k in keep], sts, dump
 
 
+# 8 entries: a small value region (the kernel's batch tail folds and snapshots it); 4096: a large one
+# (the prologue snapshot and the replica fold launch)
+@pytest.mark.parametrize("entries", [8, 4096])
 @pytest.mark.parametrize("marked", [set(), {2}, {0, 3}, {5}], ids=["clean", "middle", "first_and_later", "last"])
-def test_async_stream_equals_oracle_hostsim(hostsim_lib, oracle_lib, marked):
+def test_async_stream_equals_oracle_hostsim(hostsim_lib, oracle_lib, marked, entries):
     prog = prog_mixed()
     bs = batches(6, 512, marked)
-    ver_o, dump_o = oracle_stream(oracle_lib, prog, bs)
-    ver_a, st_a, dump_a = host_stream(hostsim_lib, prog, bs, True)
-    ver_s, st_s, dump_s = host_stream(hostsim_lib, prog, bs, False)
+    ver_o, dump_o = oracle_stream(oracle_lib, prog, bs, entries)
+    ver_a, st_a, dump_a = host_stream(hostsim_lib, prog, bs, True, entries=entries)
+    ver_s, st_s, dump_s = host_stream(hostsim_lib, prog, bs, False, entries=entries)
     assert dump_a == dump_o == dump_s
     for b in range(len(bs)):
         assert (ver_a[b] == ver_o[b]).all() and (ver_s[b] == ver_o[b]).all(), f"batch {b}"
@@ -109,6 +112,38 @@ def test_async_map_access_completes_pipeline(hostsim_lib):
     vm.close()
 
 
+def host_update_between(lib, prog, bs, kind, entries):
+    """Batches with a host map update between them (the staged snapshot must not outlive it); kind:
+    "oracle" (run_batch on the oracle), "sync" or "async" (device entry points on host memory)."""
+    vm = VM(Settings(), lib=lib)
+    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, entries))
+    vm.set_entrypoint(vm.add_raw_program(prog))
+    for b, (u, d) in enumerate(bs):
+        u = u.copy()
+        if kind == "async":
+            vm.run_batch_device_async(u.ctypes.data, u.nbytes, d.ctypes.data, len(d))
+        elif kind == "oracle":
+            vm.run_batch(u, d, want_regs=False)
+        else:
+            vm.run_batch_device(u.ctypes.data, u.nbytes, d.ctypes.data, len(d))
+        if b == 1:
+            vm.map_update(m, np.uint32(3).tobytes(), np.arange(16, dtype=np.uint8).tobytes())
+    dump = vm.map_dump(m)
+    vm.close()
+    return dump
+
+
+@pytest.mark.parametrize("entries", [8, 4096])
+def test_async_host_update_between_batches(hostsim_lib, oracle_lib, entries):
+    """A host map update between pipelined batches reaches the later batches and their rollback points:
+    a replayed batch after the update starts from the updated value."""
+    prog = prog_mixed()
+    bs = batches(4, 256, {3})
+    want = host_update_between(oracle_lib, prog, bs, "oracle", entries)
+    assert host_update_between(hostsim_lib, prog, bs, "sync", entries) == want
+    assert host_update_between(hostsim_lib, prog, bs, "async", entries) == want
+
+
 def test_async_delta_needs_sync_batch(hostsim_lib):
     """Shard deltas are taken against a synchronous batch's start: refused after pipelined batches."""
     from gobpfld_amd.emulator import EmulatorError
@@ -129,14 +164,15 @@ def test_async_delta_needs_sync_batch(hostsim_lib):
 
 # ------------------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
+@pytest.mark.parametrize("entries", [8, 4096])
 @pytest.mark.parametrize("marked", [set(), {2}, {0, 3}], ids=["clean", "middle", "first_and_later"])
-def test_async_stream_equals_oracle_gpu(gpu_lib, oracle_lib, marked):
+def test_async_stream_equals_oracle_gpu(gpu_lib, oracle_lib, marked, entries):
     import torch
     prog = prog_mixed()
     bs = batches(6, 4096, marked)
-    ver_o, dump_o = oracle_stream(oracle_lib, prog, bs)
+    ver_o, dump_o = oracle_stream(oracle_lib, prog, bs, entries)
     vm = VM(Settings(), lib=gpu_lib)
-    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, 8))
+    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, entries))
     vm.set_entrypoint(vm.add_raw_program(prog))
     dev, hs = [], []
     for u, d in bs:
@@ -176,3 +212,55 @@ def test_async_c2_full_size_stream(gpu_lib):
     assert out[True][0] == out[False][0]
     assert (out[True][1] == out[False][1]).all()
     assert out[True][2] == out[False][2] and out[True][3] == out[False][3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("entries", [8, 4096])
+def test_async_host_update_between_batches_gpu(gpu_lib, oracle_lib, entries):
+    """On the device: a host map update between pipelined batches reaches the later batches and the
+    rollback point of a replayed one."""
+    import torch
+    prog = prog_mixed()
+    bs = batches(4, 4096, {3})
+    want = host_update_between(oracle_lib, prog, bs, "oracle", entries)
+    vm = VM(Settings(), lib=gpu_lib)
+    m = vm.add_map(MapDef(MAP_ARRAY, 4, 16, entries))
+    vm.set_entrypoint(vm.add_raw_program(prog))
+    keep = []
+    for b, (u, d) in enumerate(bs):
+        du = torch.from_numpy(u).cuda()
+        dd = torch.from_numpy(d.view(np.uint8)).cuda()
+        keep.append((du, dd))
+        vm.run_batch_device_async(du.data_ptr(), du.numel(), dd.data_ptr(), len(d))
+        if b == 1:
+            vm.map_update(m, np.uint32(3).tobytes(), np.arange(16, dtype=np.uint8).tobytes())
+    assert vm.map_dump(m) == want
+    vm.close()
+
+
+@pytest.mark.gpu
+def test_async_c5_stream(gpu_lib):
+    """Pipelined C5 batches (a 1M-flow HASH map: prologue snapshot, no tail fold; paired adds): the
+    counters equal those of the same batches run synchronously."""
+    import torch
+    n = 1 << 20
+    umem, descs = W.build_batch("c5", 0, n)
+    d_umem = torch.from_numpy(umem).cuda()
+    d_desc = torch.from_numpy(descs.view(np.uint8)).cuda()
+    out = {}
+    for use_async in (False, True):
+        vm = VM(Settings(), lib=gpu_lib)
+        W.setup_vm(vm, "c5")
+        d_ver = torch.zeros(n, dtype=torch.int32, device="cuda")
+        run = vm.run_batch_device_async if use_async else vm.run_batch_device
+        hs = [run(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n, d_verdicts=d_ver.data_ptr()) for _ in range(4)]
+        sts = [h.stats() for h in hs] if use_async else hs
+        torch.cuda.synchronize()
+        keys, vals = vm.map_dump(1)
+        out[use_async] = (keys, vals, d_ver.cpu().numpy(), [s["status_count"] for s in sts])
+        assert all(s["mode_used"] == MODE_PARALLEL and s["conflict"] == 0 for s in sts)
+        vm.close()
+    for k in range(3):
+        assert np.array_equal(out[True][k], out[False][k])
+    assert out[True][3] == out[False][3]
+    assert int(out[True][1].view(np.uint64).reshape(-1, 2)[:, 0].sum()) > 0

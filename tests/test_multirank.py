@@ -17,7 +17,11 @@ from gobpfld_amd import workloads as W
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [("c2", 8192, None, True), ("c5", 8192, 4096, True), ("u32wrap", 64, None, True),
-         ("mixedwrap", 64, None, False), ("readvsadd", 256, None, False), ("rmw", 256, None, False)]
+         ("mixedwrap", 64, None, False), ("readvsadd", 256, None, False), ("addvsread", 256, None, True),
+         ("rmw", 256, None, False)]
+# shard epochs (several batches per exchange): a read of a field any other rank adds to needs the
+# replay, so addvsread (rank 0 reads what rank 1 adds) no longer commutes
+EPOCH_CASES = [c if c[0] != "addvsread" else (c[0], c[1], c[2], False) for c in CASES]
 
 
 def _free_port():
@@ -27,15 +31,16 @@ def _free_port():
 
 
 def _batch(name, start, n):
-    if name in ("readvsadd", "rmw"):
-        # packets [0, n/2): byte 0 = 0 (adders); [n/2, n): byte 0 = 255 (readers)
+    if name in ("readvsadd", "addvsread", "rmw"):
+        # packets [0, n/2): byte 0 = 0 (adders); [n/2, n): byte 0 = 255 (readers) — addvsread: reversed
         from gobpfld_amd._native import np_dtypes
         d_desc, _, _ = np_dtypes()
         umem = np.zeros(n * 64, dtype=np.uint8)
         descs = np.zeros(n, dtype=d_desc)
         descs["addr"] = np.arange(n) * 64
         descs["len"] = 64
-        umem[::64] = np.where(np.arange(start, start + n) >= _batch.total // 2, 255, 0)
+        second = np.arange(start, start + n) >= _batch.total // 2
+        umem[::64] = np.where(second != (name == "addvsread"), 255, 0)
         return umem, descs
     return W.build_batch("c2" if name in ("u32wrap", "mixedwrap") else name, start, n)
 
@@ -119,7 +124,7 @@ def _setup(vm, name, cap):
         vm.add_map(MapDef(MAP_ARRAY, 4, 8, 4), {0: (0xFFF0FFFFFFF0).to_bytes(8, "little")})
         vm.set_entrypoint(vm.add_raw_program(_wrap_program(name == "mixedwrap")))
         return
-    if name in ("readvsadd", "rmw"):
+    if name in ("readvsadd", "addvsread", "rmw"):
         vm.add_map(MapDef(MAP_ARRAY, 4, 8, 1))
         vm.set_entrypoint(vm.add_raw_program(_role_program(name == "rmw")))
         return
@@ -132,18 +137,17 @@ def _setup(vm, name, cap):
     vm.set_entrypoint(p)
 
 
-def _oracle(oracle_lib, name, n, cap):
-    """Single VM over the whole batch, twice (the ranks run two steps)."""
+def _oracle(oracle_lib, name, n, cap, steps=2, all_results=False):
+    """Single VM over the whole batch, `steps` times (the ranks run that many steps)."""
     from gobpfld_amd.emulator import VM, Settings
     ov = VM(Settings(), lib=oracle_lib)
     _setup(ov, name, cap)
     _batch.total = n
     umem, descs = _batch(name, 0, n)
-    r1 = ov.run_batch(umem.copy(), descs)
-    r2 = ov.run_batch(umem.copy(), descs)
+    rs = [ov.run_batch(umem.copy(), descs) for _ in range(steps)]
     dumps = {m: _dump(ov, m) for m in ov.map_defs}
     ov.close()
-    return r2, dumps
+    return (rs if all_results else rs[-1]), dumps
 
 
 @pytest.mark.parametrize("name,n,cap,commutes", CASES, ids=[c[0] for c in CASES])
@@ -189,3 +193,57 @@ def test_single_process_multi_equals_single_vm(oracle_lib, hostsim_lib, name, n,
     mu.close()
     for v in vms:
         v.close()
+
+
+def _rank_epoch(rank, world, port, name, n, cap, out_dir, steps):
+    import sys
+    sys.path.insert(0, ROOT)
+    from gobpfld_amd import _native as N
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import ShardEpoch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = N.Lib(os.path.join(ROOT, "tests", "hostsim", "libxdpemu_hostsim.so"), "xe_")
+    vm = VM(Settings(), lib=lib)
+    _setup(vm, name, cap)
+    shard = n // world
+    _batch.total = n
+    umem, descs = _batch(name, rank * shard, shard)
+    pk = umem.copy()
+    vers = [np.zeros(shard, dtype=np.uint32) for _ in range(steps)]
+
+    def run(s, use_async=False):
+        pk[:] = umem
+        f = vm.run_batch_device_async if use_async else vm.run_batch_device
+        return f(pk.ctypes.data, pk.size, descs.ctypes.data, shard, d_verdicts=vers[s].ctypes.data)
+
+    ep = ShardEpoch(vm, list(vm.map_defs), dist)
+    ep.begin()
+    for s in range(steps):  # pipelined and synchronous batches in one epoch
+        run(s, use_async=s % 2 == 0)
+    vm.sync()
+    x = ep.exchange([lambda s=s: run(s) for s in range(steps)])
+    np.save(os.path.join(out_dir, f"ver{rank}.npy"), np.stack(vers))
+    np.save(os.path.join(out_dir, f"exact{rank}.npy"), np.array([x["exact_sum"]]))
+    for m in vm.map_defs:
+        with open(os.path.join(out_dir, f"map{m}_r{rank}.bin"), "wb") as f:
+            f.write(_dump(vm, m))
+    vm.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,n,cap,commutes", EPOCH_CASES, ids=[c[0] for c in EPOCH_CASES])
+def test_two_rank_epoch_equals_single_vm(tmp_path, oracle_lib, built, name, n, cap, commutes):
+    """Three batches per rank in one shard epoch, one exchange: every batch's verdicts and the final
+    maps equal the oracle's single VM walking the three whole batches in order."""
+    world, steps = 2, 3
+    mp.start_processes(_rank_epoch, args=(world, _free_port(), name, n, cap, str(tmp_path), steps), nprocs=world,
+                       join=True, start_method="spawn")
+    rs, dumps = _oracle(oracle_lib, name, n, cap, steps=steps, all_results=True)
+    ver = np.concatenate([np.load(tmp_path / f"ver{r}.npy") for r in range(world)], axis=1)
+    for s in range(steps):
+        assert (ver[s] == rs[s].verdicts).all(), f"{name}: batch {s} verdicts differ from the single VM"
+    for m, want in dumps.items():
+        for r in range(world):
+            assert (tmp_path / f"map{m}_r{r}.bin").read_bytes() == want, f"rank {r} map {m}"
+    assert bool(np.load(tmp_path / "exact0.npy")[0]) == commutes

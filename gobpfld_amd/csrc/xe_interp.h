@@ -118,6 +118,14 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 #define XE_HAS_ORDERED 1
 #endif
 
+// Deferred commit (lane_commit, parallel_packets): a chunk's verdict stores and paired-add flush are
+// issued after the next chunk's prefetch instead of at the end of the chunk. The prefetch wait at the
+// top of every chunk is a vmcnt(0) (it must cover the LDS-DMA the compiler does not track): issued at
+// the end of the chunk, those stores and atomics put their completion latency on that wait.
+#ifndef XE_DEFER_COMMIT
+#define XE_DEFER_COMMIT 1
+#endif
+
 // Paired deferral of 8-byte map adds (pend_add / pend_flush): the per-program kernel enables it when
 // a packet can make more than one such add; the interpreter keeps it on.
 #ifndef XE_PAIR_ADDS
@@ -283,9 +291,15 @@ struct XeLane {
   XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
 #if XE_PAIR_ADDS
   // this packet's deferred 8-byte adds into one 16-byte block of a map value (pend_add): tag = block
-  // address | map << 48 | word mask << 56, sums of word 0 / word 1; flushed by lane_finish
+  // address | map << 48 | word mask << 56, sums of word 0 / word 1; flushed by lane_finish, or by
+  // lane_commit one chunk later (deferred commit)
   uint64_t pb_tag, pb_s0, pb_s1;
 #endif
+  // deferred commit (parallel mode, XE_DEFER_COMMIT): the last chunk's verdict, stored by lane_commit
+  // after the next chunk's prefetch is issued
+  bool defer;
+  int32_t dv_i;   // packet index, -1: nothing pending
+  uint32_t dv;
 };
 
 // ------------------------------------------------------------------ registers
@@ -2298,6 +2312,8 @@ XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   lane_stage(L, P, valid, a, l, fast, L.hdrbuf);
 }
 
+XE_DEV void lane_commit(XeLane& L, const XeParams& P);
+
 // Parallel-mode driver: wave `wave` of `nwaves` walks chunks wave, wave + nwaves, ... of XE_WAVE
 // packets (one per lane). Software-pipelined: while chunk c executes, the header window of the next
 // chunk and the descriptor of the one after are already in flight, so HBM latency overlaps the
@@ -2324,6 +2340,8 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   desc_load(P, i1, v1, r1lo, r1hi);
   uint32_t cur = 0;  // buffer of chunk c (wave-uniform)
   bool f0 = hdr_issue(P, L.hdrbuf, a0, v0);
+  L.defer = XE_DEFER_COMMIT != 0;
+  L.dv_i = -1;
   for (;;) {
     hdr_wait();  // window of chunk c and descriptor of chunk c1 (issued a whole chunk ago)
     lane_stage(L, P, v0, a0, l0, f0, L.hdrbuf + cur * XE_HDR_BUF);
@@ -2337,6 +2355,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     const bool v2 = c2 < nchunks && i2 < P.n;
     desc_load(P, i2, v2, r1lo, r1hi);
     const uint32_t abort_flags = xe_load_relaxed32(P.flags);
+    lane_commit(L, P);  // the previous chunk's verdicts and adds, behind this chunk's prefetch
     body(i0, v0);
     if (c1 >= nchunks) break;
     // a lane elsewhere needed an ordered write: this run will be discarded, stop early
@@ -2345,6 +2364,8 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     c1 = c2; i1 = i2; v1 = v2;
     cur ^= 1u;
   }
+  lane_commit(L, P);
+  L.defer = false;
   hdr_wait();  // no LDS-DMA may be outstanding when the wave retires
 }
 
@@ -2362,7 +2383,7 @@ XE_DEV void status_from_error(int e, int& status, int& code) {
 XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, int status, int code,
                         int32_t res_pc, uint64_t steps) {
 #if XE_PAIR_ADDS
-  pend_flush(L);
+  if (!L.defer) pend_flush(L);
 #endif
   if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
   if (status == XE_ST_INTERNAL_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
@@ -2377,7 +2398,10 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
       r.r0 = R0.v;
       P.results[i] = r;
     }
-    if (P.verdicts) P.verdicts[i] = uint32_t(uint64_t(R0.v));
+    if (P.verdicts) {
+      if (L.defer) { L.dv_i = int32_t(i); L.dv = uint32_t(uint64_t(R0.v)); }
+      else P.verdicts[i] = uint32_t(uint64_t(R0.v));
+    }
     if (P.regs) {
       xe_regs g;
 #pragma unroll
@@ -2410,6 +2434,15 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
 }
 
+// the stores lane_finish deferred (all lanes of the wave together)
+XE_DEV void lane_commit(XeLane& L, const XeParams& P) {
+#if XE_PAIR_ADDS
+  pend_flush(L);
+#endif
+  if (L.dv_i >= 0) P.verdicts[L.dv_i] = L.dv;
+  L.dv_i = -1;
+}
+
 // Copy the map descriptor table into LDS (all threads of the block; barrier inside): helpers read
 // map fields with LDS loads (lgkmcnt only) instead of vector global loads whose vmcnt wait would
 // also drain the header prefetch.
@@ -2435,6 +2468,9 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   L.wave = wave;
   L.awidth = 0;
   L.pend = pend;
+  L.defer = false;
+  L.dv_i = -1;
+  L.dv = 0;
 #if XE_PAIR_ADDS
   L.pb_tag = L.pb_s0 = L.pb_s1 = 0;
 #endif

@@ -22,11 +22,23 @@ defs = sys.argv[2:]
 lib = C.CDLL(str(PRODUCT_LIB))
 lib.xe_translate_uops.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
 lib.xe_jit_source.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+lib.xe_jit_source_geom.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]
 raw = np.ascontiguousarray(np.asarray(W.CONFIGS[name]["program"](), dtype=np.uint64))
 u = np.zeros(len(raw) * 16, dtype=np.uint8)
 n = lib.xe_translate_uops(raw.ctypes.data, len(raw), u.ctypes.data, len(raw))
 buf = C.create_string_buffer(1 << 22)
-lib.xe_jit_source(u.ctypes.data, n, buf, len(buf))
+# the config's real map geometry (kind, key, value, max entries, cap, key words, replicas)
+geom = []
+for mdef, _ in W.workload_maps(name):
+    if mdef.type in (1, 5):  # HASH / PERCPU_HASH
+        cap = 16
+        while cap < 2 * mdef.max_entries:
+            cap <<= 1
+        geom += [2, mdef.key_size, mdef.value_size, mdef.max_entries, cap, (mdef.key_size + 7) // 8, 1]
+    else:
+        geom += [1, mdef.key_size, mdef.value_size, mdef.max_entries, 0, 0, 16]
+g = np.asarray(geom, dtype=np.uint32)
+lib.xe_jit_source_geom(u.ctypes.data, n, g.ctypes.data, len(geom) // 7, buf, len(buf))
 src = buf.value.decode()
 out = Path("/tmp") / f"xe_jit_{name}"
 out.mkdir(exist_ok=True)

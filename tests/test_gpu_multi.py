@@ -41,3 +41,61 @@ def test_two_shards_on_one_gpu_equal_single_vm(gpu_lib, oracle_lib, name, n, cap
     mu.close()
     for v in vms:
         v.close()
+
+
+EPOCH_GPU = [("c2", 8192, None), ("c5", 8192, 4096), ("u32wrap", 64, None)]
+
+
+@pytest.mark.parametrize("name,n,cap", EPOCH_GPU, ids=[c[0] for c in EPOCH_GPU])
+def test_epoch_two_shards_on_one_gpu(gpu_lib, oracle_lib, name, n, cap):
+    """Shard epoch on the device: two VMs on cuda:0 each run three pipelined batches after
+    xe_epoch_begin; xe_shard_check over the epoch footprints, xe_map_delta against the epoch's start,
+    a device sum and xe_map_apply_delta then give both VMs the oracle's maps after the three whole
+    batches, and every batch's verdicts equal the oracle's."""
+    import torch
+    from gobpfld_amd.emulator import VM, Settings
+    G, steps = 2, 3
+    vms = [VM(Settings(device=0), lib=gpu_lib) for _ in range(G)]
+    for v in vms:
+        _setup(v, name, cap)
+    shard = n // G
+    _batch.total = n
+    host = [_batch(name, k * shard, shard) for k in range(G)]
+    dev = [(torch.from_numpy(u).cuda(), torch.from_numpy(d.view(np.uint8)).cuda()) for u, d in host]
+    vers = [[torch.zeros(shard, dtype=torch.int32, device="cuda") for _ in range(steps)] for _ in range(G)]
+    for v in vms:
+        v.epoch_begin()
+    for s in range(steps):
+        for k, v in enumerate(vms):
+            u, d = dev[k]
+            v.run_batch_device_async(u.data_ptr(), u.numel(), d.data_ptr(), shard, d_verdicts=vers[k][s].data_ptr())
+    for v in vms:
+        v.sync()
+    fps = np.concatenate([v.footprint() for v in vms])
+    ok, lanes = vms[0].shard_check(fps, G)
+    assert ok, "commuting programs must pass the epoch check"
+    for m in vms[0].map_defs:
+        lane = lanes[m - 1]
+        if not lane:
+            continue
+        nb = vms[0].map_values_bytes(m) * (2 if lane == 2 else 1)
+        bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in vms]
+        for v, b in zip(vms, bufs):
+            v.map_delta(m, b.data_ptr(), lane=lane)
+        w = {1: torch.uint8, 2: torch.int32, 4: torch.int32, 8: torch.int64}[lane]
+        tot = bufs[0].view(w) + bufs[1].view(w)
+        torch.cuda.synchronize()  # the sum runs on torch's stream, the apply on each VM's
+        for v in vms:
+            v.map_apply_delta(m, tot.view(torch.uint8).data_ptr(), lane=lane)
+    for v in vms:
+        v.epoch_end()
+    torch.cuda.synchronize()
+    rs, dumps = _oracle(oracle_lib, name, n, cap, steps=steps, all_results=True)
+    for s in range(steps):
+        ver = np.concatenate([vers[k][s].cpu().numpy().view(np.uint32) for k in range(G)])
+        assert (ver == rs[s].verdicts).all(), f"{name}: batch {s}"
+    for m, want in dumps.items():
+        for k, v in enumerate(vms):
+            assert _dump(v, m) == want, f"{name}: vm {k} map {m}"
+    for v in vms:
+        v.close()

@@ -99,3 +99,45 @@ def test_epoch_two_shards_on_one_gpu(gpu_lib, oracle_lib, name, n, cap):
             assert _dump(v, m) == want, f"{name}: vm {k} map {m}"
     for v in vms:
         v.close()
+
+
+def test_shard_epoch_bench_path_one_rank(gpu_lib, oracle_lib):
+    """The bench's N > 1 step path (ShardEpoch over torch.distributed with backend nccl = RCCL) at
+    world size 1 on cuda:0: pipelined C2 batches in an epoch, the footprint all-gather, the check and
+    the delta all-reduce leave the maps equal to the oracle's after the same batches."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import ShardEpoch
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        n, steps = 8192, 3
+        vm = VM(Settings(device=0), lib=gpu_lib)
+        _setup(vm, "c2", None)
+        _batch.total = n
+        u, d = _batch("c2", 0, n)
+        du, dd = torch.from_numpy(u).cuda(), torch.from_numpy(d.view(np.uint8)).cuda()
+        ver = torch.zeros(n, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        run = lambda: vm.run_batch_device(du.data_ptr(), du.numel(), dd.data_ptr(), n, d_verdicts=ver.data_ptr(), stream=stream)
+        ep = ShardEpoch(vm, list(vm.map_defs), dist, device=torch.device("cuda", 0), stream=stream)
+        ep.begin()
+        for _ in range(steps):
+            vm.run_batch_device_async(du.data_ptr(), du.numel(), dd.data_ptr(), n, d_verdicts=ver.data_ptr(), stream=stream)
+        vm.sync()
+        x = ep.exchange([run] * steps)
+        torch.cuda.synchronize()
+        assert x["exact_sum"]
+        rs, dumps = _oracle(oracle_lib, "c2", n, None, steps=steps, all_results=True)
+        assert (ver.cpu().numpy().view(np.uint32) == rs[-1].verdicts).all()
+        for m, want in dumps.items():
+            assert _dump(vm, m) == want
+        vm.close()
+    finally:
+        dist.destroy_process_group()

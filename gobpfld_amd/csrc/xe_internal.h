@@ -251,6 +251,9 @@ struct XeParams {
   // pipelined batches (xe_run_batch_device_async): set on the device by an earlier batch's epilogue
   // when that batch must be replayed in order; the launch then does nothing (null: synchronous run)
   const uint32_t* poison;
+  // sequential mode: stage the next 64 packets' descriptors and header windows with the whole wave
+  // (no program of the VM writes packet bytes), then run them one after another on lane 0
+  uint32_t seq_prefetch;
 };
 
 // Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in

@@ -40,6 +40,10 @@ typedef unsigned int xe_u4 __attribute__((ext_vector_type(4)));
 XE_DEV unsigned long long xe_ballot(bool p) { return __ballot(p); }
 XE_DEV int xe_readfirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 XE_DEV int xe_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+XE_DEV uint64_t xe_readlane64(uint64_t v, int l) {
+  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
+}
 XE_DEV int xe_lane() { return __lane_id(); }
 // force a loaded value to be materialised at this point (its s_waitcnt lands here)
 XE_DEV void xe_pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
@@ -80,6 +84,7 @@ struct xe_u4 {
 XE_DEV unsigned long long xe_ballot(bool p) { return p ? 1ull : 0ull; }
 XE_DEV int xe_readfirst(int v) { return v; }
 XE_DEV int xe_readlane(int v, int) { return v; }
+XE_DEV uint64_t xe_readlane64(uint64_t v, int) { return v; }
 XE_DEV int xe_lane() { return 0; }
 XE_DEV void xe_pin(uint64_t&) {}
 XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
@@ -2266,7 +2271,7 @@ XE_DEV void hdr_wait() {
 // whose descriptor (a, l) was fetched by desc_fetch and whose window was issued into buffer `buf`
 // (hdr_issue returned `fast`; hdr_wait done).
 XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uint32_t l, bool fast,
-                       XE_LP(uint8_t) buf) {
+                       XE_LP(uint8_t) buf, int col = -1) {
 #pragma unroll
   for (int r = 0; r < 10; r++) reg_replace(L, r, XE_KIND_IMM, 0, 0, 0);
   reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
@@ -2288,7 +2293,7 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   L.pkt = P.umem;
   L.plen = 0;
   L.hdr_len = 0;
-  L.hdr = buf + xe_lane() * 16;
+  L.hdr = buf + (col < 0 ? xe_lane() : col) * 16;  // col: the staged packet's column (sequential mode)
   L.hsh = fast ? int(a & 15) : 0;
   if (valid) {
     L.pkt = P.umem + a;
@@ -2316,6 +2321,39 @@ XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
 }
 
 XE_DEV void lane_commit(XeLane& L, const XeParams& P);
+
+// Sequential-mode driver (the exact in-order replay): lane 0 runs the packets one after another.
+// With P.seq_prefetch the whole wave first stages the next XE_WAVE packets (lane k: descriptor and
+// header window of packet c0 + k, the window in lane k's column), so the replay lane's per-packet
+// chain is the program's own work instead of descriptor -> window -> program round trips; without it
+// (a program may write packet bytes a later packet reads) each packet is fetched just before it runs.
+// body(i, valid) runs the staged packet on the lanes where valid and calls lane_finish (all lanes).
+template <class Body>
+XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
+  const uint32_t lane = uint32_t(xe_lane());
+  for (uint32_t c0 = 0; c0 < P.n; c0 += XE_WAVE) {
+    const uint32_t m = P.n - c0 < XE_WAVE ? P.n - c0 : XE_WAVE;
+    uint64_t a = 0;
+    uint32_t l = 0;
+    bool f = false;
+    if (P.seq_prefetch) {
+      const bool v = lane < m;
+      desc_fetch(P, c0 + lane, v, a, l);
+      f = hdr_issue(P, L.hdrbuf, a, v);
+      hdr_wait();
+    }
+#pragma unroll 1
+    for (uint32_t k = 0; k < m; k++) {
+      const bool valid = lane == 0;
+      if (P.seq_prefetch)
+        lane_stage(L, P, valid, xe_readlane64(a, int(k)), uint32_t(xe_readlane(int(l), int(k))),
+                   xe_readlane(int(f), int(k)) != 0, L.hdrbuf, int(k));
+      else
+        lane_reset(L, P, c0 + k, valid);
+      body(c0 + k, valid);
+    }
+  }
+}
 
 // Parallel-mode driver: wave `wave` of `nwaves` walks chunks wave, wave + nwaves, ... of XE_WAVE
 // packets (one per lane). Software-pipelined: while chunk c executes, the header window of the next

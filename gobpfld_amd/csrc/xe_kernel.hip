@@ -7,6 +7,8 @@
 // the multi-GPU all-reduce.
 #include "xe_interp.h"
 
+#include <hipcub/device/device_radix_sort.hpp>
+
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[4 * XE_HDR_WAVE_BYTES];
   __shared__ XePend pend_lds[4];
@@ -18,7 +20,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   wave_state_init(L, P, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, &pend_lds[threadIdx.x >> 6]);
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
-    for (uint32_t i = 0; i < P.n; i++) run_packet(L, P, i, lane == 0);
+    seq_packets(L, P, [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });
   } else {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -131,6 +133,52 @@ extern "C" __global__ void __launch_bounds__(1024) xe_tail_kernel(XeTailArgs A) 
 extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s) {
   if (A->rep_words > 256) return -1;
   hipLaunchKernelGGL(xe_tail_kernel, dim3(1), dim3(1024), 0, s, *A);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Descriptor overlap check (packet-writing programs): the reference walks the packets in order, so a
+// packet whose bytes another packet of the batch also covers sees that packet's writes when it comes
+// later. Parallel lanes cannot reproduce that; such a batch runs the in-order path. Exact: the
+// descriptors' byte ranges [addr, addr + len) (empty or outside the UMEM: none) sorted by start
+// overlap iff two neighbours do.
+__global__ void xe_desc_split_kernel(const xe_desc* d, uint32_t n, uint64_t umem_len, unsigned long long* key,
+                                     uint32_t* len) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t a = d[i].addr;
+    uint32_t l = d[i].len;
+    if (a > umem_len || uint64_t(l) > umem_len - a) l = 0;  // desc_fix: such a frame has no bytes
+    key[i] = l ? a : ~0ull;
+    len[i] = l;
+  }
+}
+__global__ void xe_desc_overlap_kernel(const unsigned long long* key, const uint32_t* len, uint32_t n, uint32_t* flag) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i + 1 < n; i += uint64_t(gridDim.x) * blockDim.x)
+    if (len[i] && len[i + 1] && key[i] + len[i] > key[i + 1]) *flag = 1u;
+}
+// scratch == nullptr: *scratch_bytes receives the size needed; otherwise *flag (device) := overlap
+extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* scratch_bytes,
+                                      uint32_t* flag, hipStream_t s) {
+  const size_t arr = ((size_t(n) * 8 + 255) & ~size_t(255)) * 2 + ((size_t(n) * 4 + 255) & ~size_t(255)) * 2;
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                         (uint32_t*)nullptr, (uint32_t*)nullptr, int(n), 0, 64, s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *scratch_bytes = arr + tmp;
+    return 0;
+  }
+  if (*scratch_bytes < arr + tmp) return -1;
+  uint8_t* p = (uint8_t*)scratch;
+  auto take = [&](size_t bytes) { uint8_t* q = p; p += (bytes + 255) & ~size_t(255); return q; };
+  unsigned long long* k0 = (unsigned long long*)take(size_t(n) * 8);
+  unsigned long long* k1 = (unsigned long long*)take(size_t(n) * 8);
+  uint32_t* l0 = (uint32_t*)take(size_t(n) * 4);
+  uint32_t* l1 = (uint32_t*)take(size_t(n) * 4);
+  const uint32_t blocks = n / 256 + 1 < 4096 ? n / 256 + 1 : 4096;
+  if (hipMemsetAsync(flag, 0, 4, s) != hipSuccess) return -1;
+  hipLaunchKernelGGL(xe_desc_split_kernel, dim3(blocks), dim3(256), 0, s, (const xe_desc*)desc, n, umem_len, k0, l0);
+  if (hipcub::DeviceRadixSort::SortPairs(p, tmp, k0, k1, l0, l1, int(n), 0, 64, s) != hipSuccess) return -1;
+  hipLaunchKernelGGL(xe_desc_overlap_kernel, dim3(blocks), dim3(256), 0, s, k1, l1, n, flag);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

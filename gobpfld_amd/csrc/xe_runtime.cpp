@@ -34,6 +34,8 @@ extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, ui
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
 extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s);
+extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* scratch_bytes,
+                                      uint32_t* flag, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
                             bool* general, const char** err);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -64,7 +66,7 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   if (P->mode == XE_MODE_PARALLEL) {
     parallel_packets(L, *P, 0, 1, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
   } else {
-    for (uint32_t i = 0; i < P->n; i++) run_packet(L, *P, i, true);
+    seq_packets(L, *P, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
   }
   flush_wave_state(L, *P);
   return 0;
@@ -149,6 +151,22 @@ int launch_tail(const XeTailArgs* A, xe_stream_t) {  // xe_kernel.hip xe_tail_ke
 int host_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
 void host_free(void* p) { free(p); }
 int host_device_ptr(void** d, void* h) { *d = h; return 0; }
+int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
+                        xe_stream_t) {  // xe_kernel.hip xe_launch_desc_overlap
+  if (!scratch) { *bytes = 8; return 0; }
+  std::vector<std::pair<uint64_t, uint32_t>> r;
+  const xe_desc* d = (const xe_desc*)desc;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t l = d[i].len;
+    if (d[i].addr > umem_len || uint64_t(l) > umem_len - d[i].addr) l = 0;
+    if (l) r.emplace_back(d[i].addr, l);
+  }
+  std::sort(r.begin(), r.end());
+  *flag = 0;
+  for (size_t i = 0; i + 1 < r.size(); i++)
+    if (r[i].first + r[i].second > r[i + 1].first) *flag = 1;
+  return 0;
+}
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
@@ -187,6 +205,10 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
 int host_alloc(void** p, size_t n) { return hipHostMalloc(p, n ? n : 8, hipHostMallocDefault) == hipSuccess ? 0 : -1; }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
+int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
+                        xe_stream_t s) {
+  return xe_launch_desc_overlap(desc, n, umem_len, scratch, bytes, flag, s);
+}
 // device-visible address of pinned host memory (hipHostMalloc default: mapped, coherent)
 int host_device_ptr(void** d, void* h) { return hipHostGetDevicePointer(d, h, 0) == hipSuccess ? 0 : -1; }
 struct Timer {
@@ -545,6 +567,7 @@ struct xe_vm {
   // host-run staging
   void* d_umem = nullptr; size_t d_umem_cap = 0;
   void* d_usnap = nullptr; size_t d_usnap_cap = 0;  // packet bytes before a replayable parallel pass
+  void* d_ovl = nullptr; size_t d_ovl_cap = 0;      // descriptor overlap check: sort scratch + flag
   void* d_desc = nullptr; size_t d_desc_cap = 0;
   void* d_res = nullptr; size_t d_res_cap = 0;
   void* d_ver = nullptr; size_t d_ver_cap = 0;
@@ -1387,7 +1410,11 @@ static bool may_write_packet(const std::vector<XeUop>& prog) {
             if (reg(u.dst) & T_PKT) return true;
             if (u.cls == U_STX && (reg(u.dst) & (T_CTX | T_FRM))) spilled |= reg(u.src);
             break;
-          case U_HELPER: set(0, 0); break;  // R0 := map value pointer or scalar
+          case U_HELPER:
+            if (u.imm == 12) return true;                      // tail call: another program runs on
+            if (u.imm == 88 && (reg(2) & T_PKT)) return true;  // pop writes the element through R2
+            set(0, 0);                                         // R0 := map value pointer or scalar
+            break;
           default: break;                   // NOP, NEG, END, LDIMM64 (in place: taint kept)
         }
         for (int k = 0; k < 2; k++) {
@@ -1626,6 +1653,20 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   const bool keep_pkts = mode == XE_MODE_AUTO && umem_len && may_write_packet(vm->programs[vm->entry]);
   if (keep_pkts && (ensure_buf(&vm->d_usnap, &vm->d_usnap_cap, umem_len) || d2d(vm->d_usnap, d_umem, umem_len, s)))
     return fail(vm, XE_ERR_DEVICE, "packet snapshot");
+  // A packet-writing program over descriptors whose bytes overlap: in the reference's order a later
+  // packet reads what an earlier one wrote, which parallel lanes cannot reproduce; in order straight away.
+  bool overlap = false;
+  if (keep_pkts && n > 1) {
+    size_t need = 0;
+    uint32_t flag = 0;
+    if (launch_desc_overlap(d_desc, n, umem_len, nullptr, &need, nullptr, s) ||
+        ensure_buf(&vm->d_ovl, &vm->d_ovl_cap, need + 256))
+      return fail(vm, XE_ERR_DEVICE, "device alloc (descriptor overlap check)");
+    uint32_t* d_flag = (uint32_t*)((uint8_t*)vm->d_ovl + ((need + 255) & ~size_t(255)));
+    if (launch_desc_overlap(d_desc, n, umem_len, vm->d_ovl, &need, d_flag, s) || d2h(&flag, d_flag, 4, s) || dsync(s))
+      return fail(vm, XE_ERR_DEVICE, "descriptor overlap check");
+    overlap = flag != 0;
+  }
   std::vector<unsigned long long> aux(aux_used);
   std::vector<unsigned long long> red;
   // sum / OR the per-wave replicas: [0] flags, replica r at 16 + r * rep_words
@@ -1675,6 +1716,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       }
       if (m.ordered() && map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
     }
+    // the replay lane's packets are staged 64 at a time by the whole wave unless a packet may write
+    // packet bytes a later packet reads (its window must then be fetched after the earlier writes)
+    P.seq_prefetch = may_write_packet(vm->programs[vm->entry]) ? 0u : 1u;
     for (int attempt = 0;; attempt++) {
       P.mode = XE_MODE_SEQUENTIAL;
       if (general && ensure_arena(vm, true, 1, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (replay arena)");
@@ -1697,7 +1741,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
   float kms = 0;
-  if (mode == XE_MODE_SEQUENTIAL || (mode == XE_MODE_AUTO && has_ordered_maps(vm))) {
+  if (mode == XE_MODE_SEQUENTIAL || (mode == XE_MODE_AUTO && has_ordered_maps(vm)) || overlap) {
     // ordered maps: every operation on them is order-dependent; replay straight away
     used = XE_MODE_SEQUENTIAL;
     if (int rc = sequential(kms)) return rc;

@@ -3,10 +3,12 @@
 
 Default workload (N=1) = BASELINE configs[1], "C2": ~40-insn L2/L3 classifier over 16,777,216 x 64 B
 synthetic packets with per-proto ARRAY counters. A step = one pass of the batch through the emulator
-(xe_run_batch_device: map snapshot, interpreter kernel, commutativity check) with packets, descriptors
-and the verdict buffer already resident in HBM. For N>1 (torchrun, one rank per GPU) every rank runs
-its own 16M-packet shard (weak scaling) and the counter map deltas are all-reduced over RCCL inside
-the step. Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
+(a pipelined xe_run_batch_device_async: the per-program kernel, then the one-block epilogue with the
+device-side commutativity check; --sync: xe_run_batch_device) with packets, descriptors and the
+verdict buffer already resident in HBM. For N>1 (torchrun, one rank per GPU) every rank runs its own
+16M-packet shard (weak scaling); the timed steps form one shard epoch whose counter map deltas are
+all-reduced over RCCL (or replayed in order) inside the timed region. Prints ONE JSON line (rank 0)
+with roofline and cpu_baseline objects.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--packets P]
 """
@@ -276,8 +278,12 @@ def main() -> None:
         return single_process_multi(args, args.config, n1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on one GPU (scripts/rehearse_multi.sh): every rank on one device,
+    # the exchange over gloo (RCCL refuses two ranks on one GPU); timings from such a run mean nothing
+    if os.environ.get("XE_BENCH_REHEARSE"):
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if os.environ.get("XE_BENCH_REHEARSE") else "nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

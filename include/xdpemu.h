@@ -242,14 +242,17 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
 /* Pipelined form of xe_run_batch_device for a stream of batches (a serving loop): enqueues the batch
  * behind those still in flight on the same stream and returns without waiting. The observable result
  * is exactly that of calling xe_run_batch_device for each batch in submission order: each batch's
- * conflict check runs on the device at its end (an epilogue kernel); a batch that must be replayed in
+ * conflict check runs on the device at its end (a one-block epilogue launch that also writes the
+ * batch's records straight into pinned host memory and, for value regions up to 16 KB, folds the
+ * replicas and snapshots the next batch's rollback point); a batch that must be replayed in
  * packet order stops the batches queued behind it from running, and xe_sync (or the next call that
  * needs the VM's state) rolls the maps back to that batch's start and re-runs it and its successors
  * through the synchronous path. *stats is filled when the batch completes: keep it (and the batch
  * buffers) valid until xe_sync returns. Batches that cannot pipeline (sequential mode, ordered maps,
  * programs that may write packet bytes) run synchronously after everything in flight. Every other
  * entry point that reads or changes VM state completes the pipelined batches first. After pipelined
- * batches, xe_map_delta / xe_map_apply_delta need a synchronous batch first (their base snapshot).
+ * batches, xe_map_delta / xe_map_apply_delta need a synchronous batch first (their base snapshot)
+ * unless a shard epoch is open (xe_epoch_begin). Up to 3 batches are in flight per VM.
  * Not a reference entry point: the Go harness runs one packet at a time. */
 int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                               void* d_results, void* d_verdicts, void* d_regs, void* stream,
@@ -258,7 +261,10 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
 int xe_sync(xe_vm* vm);
 /* Host-memory form (end-to-end: pinned staging + hipMemcpyAsync H2D/D2H). Packet writes made by the
  * program are copied back into umem (only when the program can write packet memory at all: a
- * may-point-to analysis of the program at load). results/regs may be NULL. */
+ * may-point-to analysis of the program at load). results/regs may be NULL.
+ * For a program that may write packet bytes, a batch whose descriptors cover overlapping bytes runs
+ * in packet order (XE_MODE_AUTO; an exact check over the sorted byte ranges): in the reference's
+ * loop a later packet reads what an earlier one wrote. */
 int xe_run_batch_host(xe_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* desc, uint32_t n,
                       xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats);
 

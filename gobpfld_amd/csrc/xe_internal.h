@@ -174,6 +174,67 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 #define XE_FLAG_ORDERED 1u   // a lane needed a non-commutative map write in parallel mode
 #define XE_FLAG_CAPACITY 2u   // a lane ran out of its arena (general model): the host replays with more
 #define XE_FLAG_UNALIGNED 4u  // a map add not aligned to its own width (cross-shard delta lanes inexact)
+#define XE_FLAG_KEYED 8u      // XE_MODE_SPEC: a packet's ARRAY / HASH write was held back (its key logged)
+
+// ---------------------------------------------------------------- keyed ordered execution
+// Kernel-internal modes of the keyed path (xe_runtime.cpp keyed_run, xe_interp.h key_touch). A batch
+// whose packets write map entries runs, instead of on one lane in packet order:
+//   XE_MODE_SPEC   every packet in parallel against the batch's start state, its ARRAY / HASH writes
+//                  held back; each packet logs the map keys it touches (read / add / write);
+//   (build)        the keys some packet writes form the set D; packets touching a D key are joined
+//                  into chains (connected components over their D keys), each chain sorted in packet
+//                  order; absent HASH keys of D get a reserved slot record (tombstone + key words);
+//   XE_MODE_PARALLEL + skip: the packets on no chain, in parallel (they only read / add keys nobody
+//                  writes: commutative, checked by the usual footprints);
+//   XE_MODE_CHAIN  one lane per chain, in packet order, writes applied. Every key a chain packet
+//                  touches must be a key of its own chain, and every key it writes must be in D;
+//                  anything else aborts (XE_FLAG_ORDERED) and the batch is replayed on one lane.
+// Keys of different chains never meet, so the result is the reference's packet order.
+#define XE_MODE_SPEC 16u
+#define XE_MODE_CHAIN 17u
+#define XE_KLOG 4u            // keys a packet may touch (more: the batch takes the one-lane replay)
+#define XE_SLOT_BUSY 8u       // a slot record being reserved (key words not yet written)
+#define XE_INS_WORDS 9u       // insert-log entry: map index, then the zero-padded key words
+
+// key id of map m's key: 6 bits of map index, 56 bits of a mixed key hash, bit 1 set (never 0), bit 0
+// clear (the key log uses it as the "written" mark)
+XE_HD uint64_t xe_kid_mix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
+  return (uint64_t(m & 63u) << 58) | (xe_kid_mix(h) & ((1ull << 58) - 4ull)) | 2ull;
+}
+// build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
+enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_STARTS, XE_KS_RESERVE };
+#define XE_KID_ARRAY_TAG 0xA7A7A7A700000000ull
+#define XE_KID_NIL_KEY 0x6e696c6b65790001ull  // the nil (empty) hash key
+
+struct XeKeyed {
+  uint64_t* klog;      // [n * XE_KLOG] key ids a packet touched (| 1: written)
+  uint32_t* kcnt;      // [n] keys the packet touched (> XE_KLOG: overflow)
+  uint64_t* ins;       // insert log: [ins_cap * XE_INS_WORDS], entries of held-back HASH inserts
+  uint32_t* nins;      // entries appended
+  uint32_t ins_cap;
+  uint32_t dcap;       // D table slots (power of two)
+  uint64_t* dkid;      // D table: key ids (0 = free)
+  uint32_t* dcomp;     // D table: chain (union-find parent, then the root)
+  uint32_t* drep;      // D table: the insert-log entry that reserves the key (XE_NONE: none yet)
+  uint32_t* dcount;    // [64] D keys per map (HASH capacity bound)
+  uint32_t* err;       // build errors: 1 = key log overflow, 2 = no slot for a reservation, 4 = insert without D key
+  uint32_t* changed;   // union-find round changed something
+  uint32_t* ckey;      // [n] chain of packet i (dcap: none)
+  uint32_t* okey;      // [n] sorted chain keys
+  uint32_t* order;     // [n] packet indices sorted by chain, in packet order within a chain
+  uint32_t* cbeg;      // [n] start of each chain in order[]
+  uint32_t* counts;    // [0] packets on chains, [1] chains
+  const uint8_t* skip; // [n] 1 = the packet runs on a chain (the parallel pass leaves it out)
+  uint32_t nO, nchains;
+};
 
 // General lane model (xe_interp.h, XE_GEN): the Go object model without fixed limits, per lane in a
 // device arena. Lanes are interleaved (element e of lane l at [e * nl + l]) so the lanes of a wave
@@ -254,6 +315,8 @@ struct XeParams {
   // sequential mode: stage the next 64 packets' descriptors and header windows with the whole wave
   // (no program of the VM writes packet bytes), then run them one after another on lane 0
   uint32_t seq_prefetch;
+  // keyed ordered execution (XE_MODE_SPEC / XE_MODE_CHAIN, and the skip mask of its parallel pass)
+  XeKeyed K;
 };
 
 // Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in

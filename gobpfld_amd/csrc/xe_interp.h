@@ -72,6 +72,20 @@ XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) {
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) {
   return __hip_atomic_load((XE_GP(unsigned int))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
+  __hip_atomic_compare_exchange_strong((XE_GP(unsigned long long))p, &c, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return c;
+}
+XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
+  return __hip_atomic_fetch_min((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV unsigned long long xe_load_acquire64(unsigned long long* p) {
+  return __hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+XE_DEV void xe_store_release64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((XE_GP(unsigned long long))p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 #else
 #define XE_DEV static inline
 #define XE_WAVE 1
@@ -93,6 +107,17 @@ XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { __atomic_fetch_or(
 XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
 XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
+  __atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+  return c;
+}
+XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
+  unsigned int o = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v < o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+  return o;
+}
+XE_DEV unsigned long long xe_load_acquire64(unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+XE_DEV void xe_store_release64(unsigned long long* p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 #endif
 
 #if defined(XE_MEM_FIELDS)
@@ -135,6 +160,13 @@ XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(
 // a packet can make more than one such add; the interpreter keeps it on.
 #ifndef XE_PAIR_ADDS
 #define XE_PAIR_ADDS 1
+#endif
+
+// Keyed ordered execution (XE_MODE_SPEC / XE_MODE_CHAIN, xe_internal.h): compiled into the interpreter
+// and the host simulation; a per-program kernel builds it only into its keyed variant, so the kernel
+// of the parallel fast path carries none of its registers.
+#ifndef XE_KEYED
+#define XE_KEYED 1
 #endif
 
 // maps whose read / atomic footprints a lane keeps in registers (the rest OR straight into the wave's
@@ -305,6 +337,15 @@ struct XeLane {
   bool defer;
   int32_t dv_i;   // packet index, -1: nothing pending
   uint32_t dv;
+#if XE_KEYED
+  // keyed ordered execution: the keys the current packet touched (XE_MODE_SPEC, written out by
+  // lane_finish; bit 0 = written), how many, whether a write was held back, and the lane's chain
+  // (XE_MODE_CHAIN)
+  uint64_t klog[XE_KLOG];
+  uint32_t kn;
+  bool kwr;
+  uint32_t kchain;
+#endif
 };
 
 // ------------------------------------------------------------------ registers
@@ -708,6 +749,91 @@ XE_DEV void fp_record(XeLane& L, const XeParams& P, uint32_t m, bool atomic, uin
   }
 }
 
+// ------------------------------------------------------------------ keyed ordered execution
+// (xe_internal.h XE_MODE_SPEC / XE_MODE_CHAIN)
+XE_DEV bool xe_concurrent(const XeParams& P) { return P.mode != XE_MODE_SEQUENTIAL; }
+
+#if XE_KEYED
+// key ids: HASH keys by their zero-padded words (the nil key has its own), ARRAY keys by element index
+XE_DEV uint64_t kid_hash(uint32_t m, const XeDevMap& M, const uint64_t* kw, bool empty) {
+  return xe_kid(m, empty ? XE_KID_NIL_KEY : xe_hash_words(kw, M.kwords, M.key_size));
+}
+XE_DEV uint64_t kid_array(uint32_t m, uint64_t elem) { return xe_kid(m, XE_KID_ARRAY_TAG ^ elem); }
+// the key of HASH slot `slot` (its record's key words; slot cap is the nil key's)
+XE_DEV uint64_t kid_slot(uint32_t m, const XeDevMap& M, uint32_t slot) {
+  if (slot == M.cap) return xe_kid(m, XE_KID_NIL_KEY);
+  uint64_t kw[XE_MAX_KEY / 8];
+  XE_GP(const uint64_t) r = (XE_GP(const uint64_t))M.keys + uint64_t(slot) * M.rwords + 1;
+#pragma unroll
+  for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w < M.kwords ? r[w] : 0;
+  return xe_kid(m, xe_hash_words(kw, M.kwords, M.key_size));
+}
+
+// D table (the keys some packet writes): open addressing over key ids, 0 = free
+XE_DEV int64_t dset_find(const XeKeyed& K, uint64_t kid) {
+  uint32_t idx = uint32_t(kid >> 2) & (K.dcap - 1);
+#pragma unroll 1
+  for (uint32_t p = 0; p < K.dcap; p++) {
+    const uint64_t k = ((XE_GP(const uint64_t))K.dkid)[idx];
+    if (k == kid) return int64_t(idx);
+    if (k == 0) return -1;
+    idx = (idx + 1) & (K.dcap - 1);
+  }
+  return -1;
+}
+
+XE_DEV bool keyed_dset_insert(const XeKeyed& K, uint64_t kid);
+
+// A map key the lane's packet touches (read / add: write = false; an ARRAY / HASH write: true).
+// SPEC: log it (repeats fold into one entry). CHAIN: a key of D must belong to the lane's chain, a
+// key outside D must not be written; otherwise the packet has left what the schedule proved
+// independent and the batch takes the one-lane replay (XE_EV_ORD). *dkey: the key is the chain's own
+// (its accesses are ordered by the chain: no footprints, adds applied in place).
+XE_DEV int key_touch(XeLane& L, const XeParams& P, uint64_t kid, bool write, bool* dkey = nullptr) {
+  if (dkey) *dkey = false;
+  if (P.mode == XE_MODE_SPEC) {
+    bool found = false;
+#pragma unroll
+    for (uint32_t j = 0; j < XE_KLOG; j++) {
+      if (j < L.kn && (L.klog[j] & ~1ull) == kid) {
+        found = true;
+        if (write) L.klog[j] |= 1ull;
+      }
+    }
+    if (!found) {
+#pragma unroll
+      for (uint32_t j = 0; j < XE_KLOG; j++)
+        if (j == L.kn) L.klog[j] = kid | (write ? 1ull : 0ull);
+      L.kn++;
+    }
+    if (write) L.kwr = true;
+    return 0;
+  }
+  if (P.mode == XE_MODE_CHAIN) {
+    const int64_t d = dset_find(P.K, kid);
+    if (d < 0) return write ? XE_EV_ORD : 0;
+    if (((XE_GP(const uint32_t))P.K.dcomp)[d] != L.kchain) return XE_EV_ORD;
+    if (dkey) *dkey = true;
+  }
+  return 0;
+}
+// the ARRAY elements [off, off + size) of map m spans (a value pointer covers the whole array)
+XE_DEV int key_touch_array(XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, int64_t off, int64_t size, bool write,
+                           bool* dkey = nullptr) {
+  if (M.value_size == 0 || size <= 0) return 0;
+  const uint64_t lo = uint64_t(off) / M.value_size, hi = uint64_t(off + size - 1) / M.value_size;
+  bool all = true;
+#pragma unroll 1
+  for (uint64_t e = lo; e <= hi; e++) {
+    bool d = false;
+    if (int r = key_touch(L, P, kid_array(m, e), write, &d)) return r;
+    all = all && d;
+  }
+  if (dkey) *dkey = all;
+  return 0;
+}
+#endif
+
 // ------------------------------------------------------------------ ByteMemory access
 struct XeBMem {
   uint8_t* base;
@@ -770,6 +896,19 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   return true;
 }
 
+#if XE_KEYED
+// the keys of an access to map memory B (handle h) at [off, off + size) (keyed modes only)
+XE_DEV int key_touch_mem(XeLane& L, const XeParams& P, uint32_t h, const XeBMem& B, int64_t off, int64_t size, bool write,
+                         bool* dkey = nullptr) {
+  if (dkey) *dkey = false;
+  if (!B.map || (P.mode != XE_MODE_SPEC && P.mode != XE_MODE_CHAIN)) return 0;
+  const XeDevMap M = map_desc(L, B.map);
+  if (B.array) return key_touch_array(L, P, B.map, M, off, size, write, dkey);
+  if (M.kind != XE_DM_HASH) return 0;  // the ordered maps never run keyed
+  return key_touch(L, P, kid_slot(B.map, M, xe_h_slot(h)), write, dkey);
+}
+#endif
+
 #if XE_GEN
 // Give private ByteMemory k its own copy of the bytes it has been reading through to (its source as
 // it is now, which is what Registers.Clone copied at call time, registers.go:233-240: every write to
@@ -782,7 +921,7 @@ XE_COLD int bm_materialize(XeLane& L, const XeParams& P, uint32_t k) {
   if (*bm_field(L, k, XE_BM_SRC) == XE_NONE || *bm_field(L, k, XE_BM_MAT) != XE_NONE) return 0;  // collected meanwhile
   XeBMem S;
   bmem_resolve(L, P, *bm_field(L, k, XE_BM_SRC), S);
-  if (P.mode == XE_MODE_PARALLEL && S.map) return XE_EV_ORD;
+  if (xe_concurrent(P) && S.map) return XE_EV_ORD;
   XE_GP(uint8_t) d = lane_bytes(L) + at;
 #pragma unroll 1
   for (uint32_t i = 0; i < n; i++) d[i] = ((XE_GP(const uint8_t))S.base)[i];
@@ -1109,7 +1248,11 @@ XE_DEV int mem_read(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int s
   XeBMem B;
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
-  if (track && B.map) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, size));
+  bool own = false;
+#if XE_KEYED
+  if (int e = key_touch_mem(L, P, h, B, off, size, false, &own)) return e;
+#endif
+  if (track && B.map && !own) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, size));
   val = int64_t(load_le(B.base + off, size));
   kind = XE_KIND_IMM;
   oh = 0;
@@ -1143,6 +1286,10 @@ XE_DEV int mem_write(XeLane& L, const XeParams& P, uint32_t h, int64_t off, int 
   bmem_resolve(L, P, h, B);
   if (int e = bounds(off, size, B.len)) return e;
   if (P.mode == XE_MODE_PARALLEL && B.map) return XE_EV_ORD;  // non-commutative shared write
+#if XE_KEYED
+  if (int e = key_touch_mem(L, P, h, B, off, size, true)) return e;
+  if (P.mode == XE_MODE_SPEC && B.map) return 0;  // held back: its key is logged as written
+#endif
 #if XE_GEN
   if (int e = bm_prepare_write(L, P, h)) return e;
   bmem_resolve(L, P, h, B);
@@ -1203,7 +1350,12 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, const XeReg& R, int64_t 
   bmem_resolve(L, P, h, B);
   if (off < 0 || xe_wadd(off, count) > B.len) return XE_E_OOB;
   if (count < 0) return XE_EV_PANIC | XE_P_MAKESLICE;
-  if (count > 0 && B.map) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, int(count)));
+  bool own = false;
+#if XE_KEYED
+  if (count > 0)
+    if (int e = key_touch_mem(L, P, h, B, off, count, false, &own)) return e;
+#endif
+  if (count > 0 && B.map && !own) fp_record(L, P, B.map, false, fp_bits(map_desc(L, B.map), B.array, off, int(count)));
 #pragma unroll 1
   for (int64_t i = 0; i < count; i++) emit(i, ((XE_GP(const uint8_t))B.base)[off + i]);
   return 0;
@@ -1288,7 +1440,7 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
         for (uint32_t k = 0; k < XE_MAX_KEY / 8; k++)
           if (k < M.kwords) eq = eq && (w[g * M.rwords + k + 1] == kw[k]);
         hit |= uint32_t(full && eq) << g;
-        stop |= uint32_t(!full && !(XE_HAS_ORDERED && (st & XE_SLOT_TOMB))) << g;
+        stop |= uint32_t(!full && !(st & XE_SLOT_TOMB)) << g;
       }
       const uint32_t act = (hit | stop) & (~0u << first);
       if (act) {
@@ -1310,7 +1462,7 @@ XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
       if (k <= M.kwords) w[k] = r[k];
     const uint32_t st = uint32_t(w[0]);
     if (!(st & XE_SLOT_FULL)) {
-      if (!XE_HAS_ORDERED || !(st & XE_SLOT_TOMB)) return -1;
+      if (!(st & XE_SLOT_TOMB)) return -1;  // tombstones: LRU evictions, keyed reservations
       idx = (idx + 1) & mask;
       continue;
     }
@@ -1341,6 +1493,65 @@ XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty
   if (M.kind == XE_DM_HASH) *M.count += 1;
   return int64_t(idx);
 }
+
+#if XE_KEYED
+// XE_MODE_CHAIN insert of an absent key: it takes the record reserved for it before the chains ran
+// (xe_keyed_reserve: a tombstone holding the key words), so no two lanes ever claim slots. -1: the
+// key has no reservation (its chain left the schedule).
+XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty) {
+  if (empty) {
+    hash_set_state(M, M.cap, XE_SLOT_FULL);
+    xe_atomic_add32(M.count, 1);
+    return int64_t(M.cap);
+  }
+  const uint32_t mask = M.cap - 1;
+  uint32_t idx = uint32_t(xe_hash_words(kw, M.kwords, M.key_size)) & mask;
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < M.cap; probe++) {
+    XE_GP(uint64_t) r = (XE_GP(uint64_t))M.keys + uint64_t(idx) * M.rwords;
+    const uint32_t st = uint32_t(r[0]);
+    if (!(st & (XE_SLOT_FULL | XE_SLOT_TOMB | XE_SLOT_BUSY))) return -1;
+    if (st & XE_SLOT_TOMB) {
+      bool eq = true;
+      for (uint32_t k = 0; k < M.kwords; k++) eq = eq && r[1 + k] == kw[k];
+      if (eq) {
+        r[0] = XE_SLOT_FULL;
+        xe_atomic_add32(M.count, 1);
+        return int64_t(idx);
+      }
+    }
+    idx = (idx + 1) & mask;
+  }
+  return -1;
+}
+
+// Reserve a record for HASH key kw of map M (one lane per distinct key; the keyed build): the key's
+// present or earlier reserved record, else the first free slot of its chain, claimed BUSY by CAS,
+// then the key words, then the tombstone state. Returns false when the table has no free slot.
+XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw) {
+  const uint32_t mask = M.cap - 1;
+  uint32_t idx = uint32_t(xe_hash_words(kw, M.kwords, M.key_size)) & mask;
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < M.cap;) {
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(M.keys + uint64_t(idx) * M.rwords);
+    const unsigned long long w0 = xe_load_acquire64(r);
+    const uint32_t st = uint32_t(w0);
+    if (st & (XE_SLOT_FULL | XE_SLOT_TOMB)) {
+      bool eq = true;
+      for (uint32_t k = 0; k < M.kwords; k++) eq = eq && ((XE_GP(const uint64_t))r)[1 + k] == kw[k];
+      if (eq) return true;
+    } else if (!(st & XE_SLOT_BUSY)) {
+      if (xe_atomic_cas64(r, w0, XE_SLOT_BUSY) != w0) continue;  // lost the slot: look at it again
+      for (uint32_t k = 0; k < M.kwords; k++) ((XE_GP(uint64_t))r)[1 + k] = kw[k];
+      xe_store_release64(r, XE_SLOT_TOMB);
+      return true;
+    }
+    idx = (idx + 1) & mask;
+    probe++;
+  }
+  return false;
+}
+#endif
 
 // read a key through a pointer register into zero-padded words; ReadRange errors give the nil key
 // (maps_hash.go:50-53). Returns a panic code or 0.
@@ -1478,6 +1689,10 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
     if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2)) return e;
+#if XE_KEYED
+    if (M.kind == XE_DM_HASH)  // the key's presence is read
+      if (int e = key_touch(L, P, kid_hash(m, M, kw, empty), false)) return e;
+#endif
 #if XE_HAS_ORDERED
     if (M.kind == XE_DM_LRU) {
       if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // a lookup promotes: a write to the UsageList
@@ -1558,6 +1773,9 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     uint32_t k, oh, al; int64_t kv;
     if (int e = mem_read(L, P, R2.h, R2.v, 4, true, k, oh, kv, al, cm2)) return in_helper(e);
     if (kv >= int64_t(M.vals_bytes)) return helper_errno_result(L, -7);
+#if XE_KEYED
+    if (int e = key_touch(L, P, kid_array(m, uint64_t(kv)), true)) return e;  // element kv is written
+#endif
 #pragma unroll 1
     for (int64_t i = 0; i < int64_t(M.value_size); i++) {
       int64_t v;
@@ -1565,6 +1783,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       int64_t dst = xe_wadd(xe_wmul(kv, int64_t(M.value_size)), i);
       if (int e = bounds(dst, 1, int64_t(M.vals_bytes))) return in_helper(e);
       if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+      if (P.mode == XE_MODE_SPEC) continue;  // held back
 #if XE_GEN
       if (int e = bm_before_write(L, P, xe_h_make(XE_H_ARRAY, m, 0))) return e;
 #endif
@@ -1577,6 +1796,10 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
     if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
+#if XE_KEYED
+    const uint64_t kid = kid_hash(m, M, kw, empty);
+    if (int e = key_touch(L, P, kid, false)) return e;  // presence (and the count) are read
+#endif
     int64_t slot = hash_find(M, kw, empty);
     if (slot < 0 && uint64_t(*M.count) + 1 > M.max_entries) return helper_errno_result(L, -7);
     if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
@@ -1584,6 +1807,25 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     int ve = ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
     if (XE_IS_PANIC(ve)) return ve;
     if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+#if XE_KEYED
+    if (int e = key_touch(L, P, kid, true)) return e;
+    if (P.mode == XE_MODE_SPEC) {  // held back; a new key goes to the insert log (its slot is reserved)
+      if (slot < 0 && keyed_dset_insert(P.K, kid)) {  // the first packet to insert the key logs it
+        const uint32_t at = xe_atomic_add32(P.K.nins, 1u);
+        if (at < P.K.ins_cap) {
+          XE_GP(uint64_t) en = (XE_GP(uint64_t))P.K.ins + uint64_t(at) * XE_INS_WORDS;
+          en[0] = uint64_t(m) | (empty ? 0x100ull : 0ull);
+#pragma unroll
+          for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) en[1 + w] = kw[w];
+        }
+      }
+      return helper_errno_result(L, 0);
+    }
+    if (slot < 0 && P.mode == XE_MODE_CHAIN) {
+      slot = hash_claim(M, kw, empty);
+      if (slot < 0) return XE_EV_ORD;
+    }
+#endif
     if (slot < 0) slot = hash_insert_new(M, kw, empty);
 #if XE_GEN
     if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, uint32_t(slot)))) return e;
@@ -1861,7 +2103,7 @@ XE_DEV int64_t ptr_eff(const XeReg& R, int32_t ioff) {
 
 // lifted read-modify-writes run as adds only where lanes run concurrently and no register record
 // could show the loaded value
-XE_DEV bool lift_active(const XeParams& P) { return P.mode == XE_MODE_PARALLEL && !P.regs; }
+XE_DEV bool lift_active(const XeParams& P) { return xe_concurrent(P) && !P.regs; }
 
 // ---- per-class handlers (exec_uop dispatches; the JIT calls them directly with constant uops)
 XE_DEV int uop_alu(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd = XE_CM_ALL) {
@@ -1951,6 +2193,9 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm
     if (XE_HAS_HASH && M.kind == XE_DM_HASH) {
       uint64_t kw[XE_MAX_KEY / 8] = {0, 0, 0, 0, 0, 0, 0, 0};
       bool empty = M.key_size > 4 || M.key_size == 0;  // ReadRange of a 4-byte tmp memory
+#if XE_KEYED
+      if (int e = key_touch(L, P, kid_hash(m, M, kw, empty), false)) return e;
+#endif
       int64_t slot = hash_find(M, kw, empty);
       if (slot < 0) return XE_E_MAP_NOT_PTR;
       reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), int64_t(u.x), 0);
@@ -1989,14 +2234,25 @@ XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd 
     if (c == XE_H_ARRAY || c == XE_H_HASH) {
       XeBMem B;
       bmem_resolve(L, P, D.h, B);
-      if (B.map) {  // the lifted read-modify-write of a map value: add the addend (lift_rmw)
+      bool own = false;  // a key of this lane's chain (XE_MODE_CHAIN): the plain store below
+#if XE_KEYED
+      if (B.map && P.mode == XE_MODE_CHAIN) {
         if (int e = bounds(off, size, B.len)) return e;
+        if (int e = key_touch_mem(L, P, D.h, B, off, size, false, &own)) return e;
+      }
+#endif
+      if (B.map && !own) {  // the lifted read-modify-write of a map value: add the addend (lift_rmw)
+        if (int e = bounds(off, size, B.len)) return e;
+#if XE_KEYED
+        if (P.mode == XE_MODE_SPEC)
+          if (int e = key_touch_mem(L, P, D.h, B, off, size, false)) return e;
+#endif
         int64_t k = int64_t(u.imm);
         if (u.x & 0xff) k = reg_get(L, int(u.x & 0xff) - 1).v;
         if (u.x & 0x100) k = int64_t(0ull - uint64_t(k));
         fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
         width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
-        wave_atomic_add_field(L, B.map, true, B.base + off, size, uint64_t(k));
+        wave_atomic_add_field(L, B.map, P.mode != XE_MODE_CHAIN, B.base + off, size, uint64_t(k));
         return 0;
       }
     }
@@ -2052,9 +2308,15 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd
     return 0;
   }
 #endif
-  fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
-  width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
-  wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL, B.base + off, size, uint64_t(S.v));
+  bool own = false;  // a key of this lane's chain: ordered by the chain, no footprint
+#if XE_KEYED
+  if (int e = key_touch_mem(L, P, h, B, off, size, false, &own)) return e;
+#endif
+  if (!own) {
+    fp_record(L, P, B.map, true, fp_bits(map_desc(L, B.map), B.array, off, size));
+    width_record(L, P, B.map, size, uint64_t(uintptr_t(B.base + off)));
+  }
+  wave_atomic_add_field(L, B.map, P.mode == XE_MODE_PARALLEL || P.mode == XE_MODE_SPEC, B.base + off, size, uint64_t(S.v));
   return 0;
 }
 
@@ -2361,6 +2623,23 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
 // interpretation instead of stalling every chunk twice (descriptor -> header). The abort flag (an
 // ordered write somewhere in the batch) is polled the same way, one chunk behind.
 // body(i, valid) runs the staged packet and calls lane_finish; all lanes call it together.
+// packet i runs in this parallel pass (the keyed path's pass leaves out the packets on chains)
+XE_DEV bool pkt_in_pass(const XeParams& P, uint32_t i) {
+#if XE_KEYED
+  if (P.K.skip && i < P.n && ((XE_GP(const uint8_t))P.K.skip)[i]) return false;
+#endif
+  return i < P.n;
+}
+// the key log of the lane's next packet starts empty
+XE_DEV void key_begin(XeLane& L) {
+#if XE_KEYED
+  L.kn = 0;
+  L.kwr = false;
+#else
+  (void)L;
+#endif
+}
+
 template <class Body>
 XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32_t nwaves, Body body) {
   const uint32_t lane = uint32_t(xe_lane());
@@ -2370,13 +2649,13 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   // an earlier pipelined batch is being replayed in order: this one re-runs afterwards
   if (P.poison && xe_readfirst(int(xe_load_relaxed32(const_cast<unsigned int*>(P.poison))))) return;
   uint32_t i0 = c * XE_WAVE + lane;
-  bool v0 = i0 < P.n;
+  bool v0 = pkt_in_pass(P, i0);
   uint64_t a0;
   uint32_t l0;
   desc_fetch(P, i0, v0, a0, l0);
   uint32_t c1 = c + nwaves;
   uint32_t i1 = c1 * XE_WAVE + lane;
-  bool v1 = c1 < nchunks && i1 < P.n;
+  bool v1 = c1 < nchunks && pkt_in_pass(P, i1);
   uint64_t r1lo, r1hi;  // raw descriptor of chunk c1, in flight
   desc_load(P, i1, v1, r1lo, r1hi);
   uint32_t cur = 0;  // buffer of chunk c (wave-uniform)
@@ -2393,10 +2672,11 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     const bool f1 = hdr_issue(P, L.hdrbuf + (cur ^ 1u) * XE_HDR_BUF, a1, v1);
     const uint32_t c2 = c1 + nwaves;
     const uint32_t i2 = c2 * XE_WAVE + lane;
-    const bool v2 = c2 < nchunks && i2 < P.n;
+    const bool v2 = c2 < nchunks && pkt_in_pass(P, i2);
     desc_load(P, i2, v2, r1lo, r1hi);
     const uint32_t abort_flags = xe_load_relaxed32(P.flags);
     lane_commit(L, P);  // the previous chunk's verdicts and adds, behind this chunk's prefetch
+    key_begin(L);
     body(i0, v0);
     if (c1 >= nchunks) break;
     // a lane elsewhere needed an ordered write: this run will be discarded, stop early
@@ -2409,6 +2689,144 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   L.defer = false;
   hdr_wait();  // no LDS-DMA may be outstanding when the wave retires
 }
+
+#if XE_KEYED
+// ---- keyed build steps, one call per item (xe_kernel.hip runs them as grids, the host simulation as
+// loops). After XE_MODE_SPEC: the D table of written keys, union-find over the D keys each packet
+// touches (rounds until nothing changes), the roots, each packet's chain (dcap: none), the chain
+// starts in the sorted order, and one slot reservation per new HASH key.
+// put key id `kid` into D; true when this call added it
+XE_DEV bool keyed_dset_insert(const XeKeyed& K, uint64_t kid) {
+  const uint32_t mask = K.dcap - 1;
+  uint32_t idx = uint32_t(kid >> 2) & mask;
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < K.dcap; probe++) {
+    const unsigned long long cur = xe_load_acquire64(reinterpret_cast<unsigned long long*>(K.dkid + idx));
+    if (cur == kid) return false;
+    if (cur == 0) {
+      const unsigned long long old = xe_atomic_cas64(reinterpret_cast<unsigned long long*>(K.dkid + idx), 0ull, kid);
+      if (old == 0) {
+        K.dcomp[idx] = idx;
+        K.drep[idx] = XE_NONE;
+        xe_atomic_add32(K.dcount + (kid >> 58), 1u);
+        return true;
+      }
+      if (old == kid) return false;
+    }
+    idx = (idx + 1) & mask;
+  }
+  xe_atomic_or32(K.err, 8u);  // D is full
+  return false;
+}
+XE_DEV void keyed_dset_item(const XeKeyed& K, uint32_t i) {
+  const uint32_t n = K.kcnt[i];
+  if (n > XE_KLOG) { xe_atomic_or32(K.err, 1u); return; }
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; j++) {
+    const uint64_t e = K.klog[uint64_t(i) * XE_KLOG + j];
+    if (e & 1ull) keyed_dset_insert(K, e & ~1ull);
+  }
+}
+XE_DEV uint32_t keyed_root(const XeKeyed& K, uint32_t x) {
+#pragma unroll 1
+  for (;;) {
+    const uint32_t p = xe_load_relaxed32(K.dcomp + x);
+    if (p == x) return x;
+    x = p;
+  }
+}
+// hook every root of packet i's D keys under the smallest (parents only decrease: rounds converge)
+XE_DEV void keyed_union_item(const XeKeyed& K, uint32_t i) {
+  const uint32_t n = K.kcnt[i] < XE_KLOG ? K.kcnt[i] : XE_KLOG;
+  if (n < 2) return;
+  uint32_t r = XE_NONE;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; j++) {
+    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
+    if (d >= 0) { const uint32_t q = keyed_root(K, uint32_t(d)); r = q < r ? q : r; }
+  }
+  if (r == XE_NONE) return;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; j++) {
+    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
+    if (d < 0) continue;
+    const uint32_t q = keyed_root(K, uint32_t(d));
+    if (q != r && xe_atomic_min32(K.dcomp + q, r) > r) xe_atomic_or32(K.changed, 1u);
+  }
+}
+XE_DEV void keyed_compress_item(const XeKeyed& K, uint32_t x) {
+  if (((XE_GP(const unsigned long long))K.dkid)[x]) K.dcomp[x] = keyed_root(K, x);
+}
+XE_DEV void keyed_assign_item(const XeKeyed& K, uint32_t i, uint8_t* skip) {
+  const uint32_t n = K.kcnt[i] < XE_KLOG ? K.kcnt[i] : XE_KLOG;
+  uint32_t c = K.dcap;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n && c == K.dcap; j++) {
+    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
+    if (d >= 0) c = K.dcomp[d];
+  }
+  K.ckey[i] = c;
+  skip[i] = c != K.dcap ? 1 : 0;
+  if (c != K.dcap) xe_atomic_add32(K.counts, 1u);
+}
+XE_DEV void keyed_starts_item(const XeKeyed& K, uint32_t p) {
+  if (p >= K.counts[0]) return;
+  if (p == 0 || K.okey[p] != K.okey[p - 1]) K.cbeg[xe_atomic_add32(K.counts + 1, 1u)] = p;
+}
+XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t e) {
+  const uint64_t* en = K.ins + uint64_t(e) * XE_INS_WORDS;
+  const uint32_t m = uint32_t(en[0] & 0xffu);
+  if (en[0] & 0x100ull) return;  // the nil key has its own slot
+  const XeDevMap M = maps[m];
+  uint64_t kw[XE_MAX_KEY / 8];
+#pragma unroll
+  for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = en[1 + w];
+  const int64_t d = dset_find(K, xe_kid(m, xe_hash_words(kw, M.kwords, M.key_size)));
+  if (d < 0) { xe_atomic_or32(K.err, 4u); return; }
+  if (xe_atomic_cas32(K.drep + d, XE_NONE, e) != XE_NONE) return;  // another entry of this key reserves it
+  if (!hash_reserve(M, kw)) xe_atomic_or32(K.err, 2u);
+}
+XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t i) {
+  switch (step) {
+    case XE_KS_DSET: keyed_dset_item(K, i); break;
+    case XE_KS_UNION: keyed_union_item(K, i); break;
+    case XE_KS_COMPRESS: keyed_compress_item(K, i); break;
+    case XE_KS_ASSIGN: keyed_assign_item(K, i, skip); break;
+    case XE_KS_IOTA: K.cbeg[i] = i; break;
+    case XE_KS_STARTS: keyed_starts_item(K, i); break;
+    case XE_KS_RESERVE: keyed_reserve_item(K, maps, i); break;
+    default: break;
+  }
+}
+
+// Chain-mode driver (XE_MODE_CHAIN, keyed ordered execution): thread g of the grid runs chains g,
+// g + nthreads, ... one after another, each chain's packets in packet order (order[cbeg[c]..] while
+// the sorted chain key stays the same). All lanes of a wave call body together until every lane of
+// the wave has run out of chains.
+template <class Body>
+XE_DEV void chain_packets(XeLane& L, const XeParams& P, uint32_t g, uint32_t nthreads, Body body) {
+  uint32_t c = g, p = 0, key = 0;
+  bool have = c < P.K.nchains;
+  if (have) { p = P.K.cbeg[c]; key = P.K.okey[p]; }
+#pragma unroll 1
+  for (;;) {
+    if (!xe_ballot(have)) break;
+    const uint32_t i = have ? P.K.order[p] : 0u;
+    L.kchain = key;
+    lane_reset(L, P, i, have);
+    key_begin(L);
+    body(i, have);
+    if (have) {
+      p++;
+      if (p >= P.K.nO || P.K.okey[p] != key) {
+        c += nthreads;
+        have = c < P.K.nchains;
+        if (have) { p = P.K.cbeg[c]; key = P.K.okey[p]; }
+      }
+    }
+  }
+}
+#endif
 
 // map an exec_uop error to the lane's final status/code
 XE_DEV void status_from_error(int e, int& status, int& code) {
@@ -2428,6 +2846,17 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 #endif
   if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
   if (status == XE_ST_INTERNAL_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
+#if XE_KEYED
+  if (P.mode == XE_MODE_SPEC) {  // the packet's key log
+    if (valid) {
+      P.K.kcnt[i] = L.kn;
+#pragma unroll
+      for (uint32_t j = 0; j < XE_KLOG; j++)
+        if (j < L.kn) P.K.klog[uint64_t(i) * XE_KLOG + j] = L.klog[j];
+    }
+    if (xe_ballot(valid && L.kwr) && xe_lane() == 0) xe_atomic_or32(P.flags, XE_FLAG_KEYED);
+  }
+#endif
   if (valid) {
     const XeReg R0 = reg_get(L, 0);
     if (P.results) {

@@ -21,6 +21,9 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
     seq_packets(L, P, [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });
+  } else if (P.mode == XE_MODE_CHAIN) {
+    chain_packets(L, P, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
+                  [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });
   } else {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -180,6 +183,37 @@ extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t ume
   if (hipcub::DeviceRadixSort::SortPairs(p, tmp, k0, k1, l0, l1, int(n), 0, 64, s) != hipSuccess) return -1;
   hipLaunchKernelGGL(xe_desc_overlap_kernel, dim3(blocks), dim3(256), 0, s, k1, l1, n, flag);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Keyed ordered execution: the build steps between the XE_MODE_SPEC pass and the chains (xe_interp.h
+// keyed_step), one grid-stride launch per step, and the sort of the packets by chain.
+extern "C" __global__ void xe_keyed_kernel(XeKeyed K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < items; i += uint64_t(gridDim.x) * blockDim.x)
+    keyed_step(K, maps, skip, step, uint32_t(i));
+}
+extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
+                               hipStream_t s) {
+  if (!items) return 0;
+  const uint32_t blocks = items / 256 + 1 < 8192 ? items / 256 + 1 : 8192;
+  hipLaunchKernelGGL(xe_keyed_kernel, dim3(blocks), dim3(256), 0, s, *K, maps, skip, step, items);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// (ckey, cbeg = 0..n-1) -> (okey, order), by chain key bits [0, end_bit); LSD radix sort is stable, so a
+// chain's packets stay in packet order. scratch == nullptr: *bytes receives the scratch size.
+extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s) {
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, int(n), 0, int(end_bit), s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *bytes = tmp;
+    return 0;
+  }
+  if (*bytes < tmp) return -1;
+  return hipcub::DeviceRadixSort::SortPairs(scratch, tmp, K->ckey, K->okey, K->cbeg, K->order, int(n), 0, int(end_bit), s) ==
+                 hipSuccess
+             ? 0
+             : -1;
 }
 
 // host-side launchers (called from xe_runtime.cpp)

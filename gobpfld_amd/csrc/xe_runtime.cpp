@@ -37,7 +37,10 @@ extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s);
 extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* scratch_bytes,
                                       uint32_t* flag, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
-                            bool* general, const char** err);
+                            bool* general, const char** err, int keyed);
+extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
+                               hipStream_t s);
+extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -63,8 +66,10 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XePend pend;
   stage_maps(L, *P, nullptr);
   wave_state_init(L, *P, 0, &pend);
-  if (P->mode == XE_MODE_PARALLEL) {
+  if (P->mode == XE_MODE_PARALLEL || P->mode == XE_MODE_SPEC) {
     parallel_packets(L, *P, 0, 1, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
+  } else if (P->mode == XE_MODE_CHAIN) {
+    chain_packets(L, *P, 0, 1, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
   } else {
     seq_packets(L, *P, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
   }
@@ -167,6 +172,18 @@ int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* s
     if (r[i].first + r[i].second > r[i + 1].first) *flag = 1;
   return 0;
 }
+int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items, xe_stream_t) {
+  for (uint32_t i = 0; i < items; i++) keyed_step(*K, maps, skip, step, i);  // xe_kernel.hip xe_keyed_kernel
+  return 0;
+}
+int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
+  if (!scratch) { *bytes = 8; return 0; }
+  std::vector<std::pair<uint32_t, uint32_t>> v(n);
+  for (uint32_t i = 0; i < n; i++) v[i] = {K->ckey[i], K->cbeg[i]};
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
+  return 0;
+}
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
@@ -203,6 +220,12 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
   return xe_launch_prologue(src, dst, words, nseg, zero, zw, s);
 }
 int host_alloc(void** p, size_t n) { return hipHostMalloc(p, n ? n : 8, hipHostMallocDefault) == hipSuccess ? 0 : -1; }
+int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items, xe_stream_t s) {
+  return xe_launch_keyed(K, maps, skip, step, items, s);
+}
+int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
+  return xe_launch_keyed_sort(K, n, end_bit, scratch, bytes, s);
+}
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
 int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
@@ -507,6 +530,36 @@ struct HostMap {
     count++;
     return idx;
   }
+  // Keyed runs leave tombstones behind (slot records reserved for a key whose chain did not insert
+  // it, xe_interp.h hash_reserve): the device probes run through them; the host mirror is rebuilt
+  // without them (same hash, fresh slots) and uploaded again before the next run. True if rebuilt.
+  bool drop_tombstones() {
+    bool any = false;
+    for (uint32_t i = 0; i < cap && !any; i++) any = (state[i] & XE_SLOT_TOMB) != 0;
+    if (!any) return false;
+    std::vector<uint32_t> full;
+    for (uint32_t i = 0; i < cap; i++)
+      if (state[i] & XE_SLOT_FULL) full.push_back(i);
+    std::vector<uint64_t> k2(full.size() * kwords);
+    std::vector<uint8_t> v2(full.size() * def.value_size);
+    std::vector<uint32_t> s2(full.size());
+    for (size_t j = 0; j < full.size(); j++) {
+      memcpy(k2.data() + j * kwords, key_at(full[j]), kwords * 8);
+      memcpy(v2.data() + j * def.value_size, vals.data() + uint64_t(full[j]) * def.value_size, def.value_size);
+      s2[j] = state[full[j]];
+    }
+    const uint32_t nil = state[cap];
+    std::fill(state.begin(), state.begin() + cap, 0u);
+    std::fill(keys.begin(), keys.begin() + uint64_t(cap) * kwords, 0ull);
+    std::fill(vals.begin(), vals.begin() + uint64_t(cap) * def.value_size, uint8_t(0));
+    count = (nil & XE_SLOT_FULL) ? 1u : 0u;
+    for (size_t j = 0; j < full.size(); j++) {
+      const int64_t at = insert(k2.data() + j * kwords);
+      state[at] = s2[j];
+      memcpy(vals.data() + uint64_t(at) * def.value_size, v2.data() + j * def.value_size, def.value_size);
+    }
+    return true;
+  }
   // linear-probing delete with backward shift (keeps probe chains intact without tombstones)
   void erase_slot(uint32_t i) {
     const uint32_t mask = cap - 1;
@@ -618,7 +671,57 @@ struct xe_vm {
   std::vector<unsigned long long> epoch_fp;
   uint32_t epoch_flags = 0;
   bool epoch_seq = false;
+  // keyed ordered execution (xe_internal.h XeKeyed): device buffers, grown on demand; keyed_hint: the
+  // last batch needed it, so the next one starts with the SPEC pass instead of a plain parallel run
+  XeKeyed kd{};
+  uint8_t* d_skip = nullptr;
+  uint32_t* d_ksmall = nullptr;  // [0..63] dcount, [64] err, [65] changed, [66..67] counts, [68] nins
+  uint64_t keyed_n = 0;          // packets the per-packet arrays hold
+  uint32_t keyed_dcap = 0, keyed_ins = 0;
+  void* d_ksort = nullptr;
+  size_t d_ksort_cap = 0;
+  bool keyed_hint = false;
+  bool keyed_refused = false;  // the keyed path refused the last order-dependent batch: go straight to the replay
 };
+// ---- keyed ordered execution buffers (XeKeyed), sized for n packets
+static void keyed_free(xe_vm* vm) {
+  XeKeyed& K = vm->kd;
+  dev_free(K.klog); dev_free(K.kcnt); dev_free(K.ins); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.drep);
+  dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.cbeg);
+  dev_free(vm->d_skip); dev_free(vm->d_ksmall); dev_free(vm->d_ksort);
+  K = XeKeyed{};
+  vm->d_skip = nullptr; vm->d_ksmall = nullptr; vm->d_ksort = nullptr;
+  vm->d_ksort_cap = 0;
+  vm->keyed_n = 0;
+  vm->keyed_dcap = vm->keyed_ins = 0;
+}
+static int keyed_alloc(xe_vm* vm, uint32_t n) {
+  if (vm->keyed_n >= n && vm->d_ksmall) return 0;
+  keyed_free(vm);
+  XeKeyed& K = vm->kd;
+  const uint64_t np = std::max<uint64_t>(n, 64);
+  uint32_t dcap = 4096;
+  while (dcap < 2 * np && dcap < (1u << 30)) dcap <<= 1;
+  const uint32_t ins = uint32_t(std::min<uint64_t>(np, 4u << 20));
+  bool bad = dev_alloc((void**)&K.klog, np * XE_KLOG * 8) || dev_alloc((void**)&K.kcnt, np * 4) ||
+             dev_alloc((void**)&K.ins, uint64_t(ins) * XE_INS_WORDS * 8) || dev_alloc((void**)&K.dkid, uint64_t(dcap) * 8) ||
+             dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4) || dev_alloc((void**)&K.drep, uint64_t(dcap) * 4) ||
+             dev_alloc((void**)&K.ckey, np * 4) || dev_alloc((void**)&K.okey, np * 4) || dev_alloc((void**)&K.order, np * 4) ||
+             dev_alloc((void**)&K.cbeg, np * 4) || dev_alloc((void**)&vm->d_skip, np) || dev_alloc((void**)&vm->d_ksmall, 128 * 4);
+  if (bad) { keyed_free(vm); return -1; }
+  K.ins_cap = ins;
+  K.dcap = dcap;
+  K.dcount = vm->d_ksmall;
+  K.err = vm->d_ksmall + 64;
+  K.changed = vm->d_ksmall + 65;
+  K.counts = vm->d_ksmall + 66;
+  K.nins = vm->d_ksmall + 68;
+  vm->keyed_n = np;
+  vm->keyed_dcap = dcap;
+  vm->keyed_ins = ins;
+  return 0;
+}
+
 
 namespace {
 
@@ -734,6 +837,7 @@ int map_download(xe_vm* vm, HostMap& m) {
   if (dsync(vm->stream)) return -1;
   m.dev_dirty = false;
   m.live = m.count;
+  if (m.dkind == XE_DM_HASH && m.drop_tombstones()) m.host_dirty = true;  // the device gets the clean layout
   return 0;
 }
 
@@ -1080,6 +1184,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
   dev_free(vm->d_usnap);
+  keyed_free(vm);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
 #ifndef XE_HOSTSIM
   if (vm->stream) (void)hipStreamDestroy(vm->stream);
@@ -1525,7 +1630,7 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
       const auto& prog = vm->programs[vm->entry];
       const char* jerr = "";
       vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
-                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &vm->jit_general, &jerr);
+                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &vm->jit_general, &jerr, 0);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
       vm->jit_nmaps = vm->maps.size();
@@ -1604,7 +1709,7 @@ void note_run(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t mo
   vm->last_fp.assign(red.begin() + 16, red.end());
   if (!vm->epoch_open) return;
   vm->epoch_flags |= vm->last_flags;
-  vm->epoch_seq = vm->epoch_seq || mode == XE_MODE_SEQUENTIAL;
+  vm->epoch_seq = vm->epoch_seq || mode == XE_MODE_SEQUENTIAL || mode == XE_MODE_KEYED;
   if (vm->epoch_fp.size() < vm->last_fp.size()) vm->epoch_fp.resize(vm->last_fp.size(), 0);
   for (size_t i = 0; i < vm->last_fp.size(); i++) vm->epoch_fp[i] |= vm->last_fp[i];
 }
@@ -1699,8 +1804,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   };
   // The exact ordered replay: one lane walks the packets in order. Its arena (and the ordered maps'
   // room) grows x4 and the replay restarts from the rollback point whenever it runs out.
-  auto sequential = [&](float& ms) -> int {
-    // rollback point of what the parallel pass never writes: hash slot records, the ordered maps
+  // rollback point of what the parallel pass never writes: hash slot records (+ counts)
+  auto snap_records = [&]() -> int {
     uint64_t kb = 0;
     for (size_t i = 1; i < vm->maps.size(); i++)
       if (vm->maps[i].dkind == XE_DM_HASH) kb += uint64_t(vm->maps[i].cap + 1) * xe_hash_rwords(vm->maps[i].kwords) * 8 + 8;
@@ -1708,12 +1813,19 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     uint64_t off = 0;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
-      if (m.dkind == XE_DM_HASH) {
-        const uint64_t rb = uint64_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8;
-        if (d2d((uint8_t*)vm->d_ksnap + off, m.d_keys, rb, s) || d2d((uint8_t*)vm->d_ksnap + off + rb, m.d_count, 4, s))
-          return fail(vm, XE_ERR_DEVICE, "snapshot");
-        off += rb + 8;
-      }
+      if (m.dkind != XE_DM_HASH) continue;
+      const uint64_t rb = uint64_t(m.cap + 1) * xe_hash_rwords(m.kwords) * 8;
+      if (d2d((uint8_t*)vm->d_ksnap + off, m.d_keys, rb, s) || d2d((uint8_t*)vm->d_ksnap + off + rb, m.d_count, 4, s))
+        return fail(vm, XE_ERR_DEVICE, "snapshot");
+      off += rb + 8;
+    }
+    return XE_OK;
+  };
+  auto sequential = [&](float& ms) -> int {
+    // rollback point of what the parallel pass never writes: hash slot records, the ordered maps
+    if (int rc = snap_records()) return rc;
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
       if (m.ordered() && map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
     }
     // the replay lane's packets are staged 64 at a time by the whole wave unless a packet may write
@@ -1737,39 +1849,161 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     }
   };
 
+  // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
+  auto fold = [&]() -> int {
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s)) return -1;
+    }
+    return 0;
+  };
+  // Keyed ordered execution (xe_internal.h): the SPEC pass, the build, the parallel pass of the packets
+  // on no chain, the chains. Returns 1 when the batch has to take the one-lane replay instead (maps,
+  // packets and records rolled back), 0 when done (used: XE_MODE_PARALLEL when no packet wrote a map
+  // entry, so the SPEC pass was an ordinary parallel run; else XE_MODE_KEYED), < 0 on error.
+  auto keyed = [&](uint32_t& used_out) -> int {
+    void* kjit = nullptr;
+#ifndef XE_HOSTSIM
+    if (jit) {  // the per-program kernel's keyed variant
+      const auto& prog = vm->programs[vm->entry];
+      bool cy = false, ge = false;
+      const char* jerr = "";
+      kjit = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
+                        uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
+      if (!kjit) return 1;
+    }
+#endif
+    auto klaunch = [&](const XeParams* p, uint32_t b) { return kjit ? launch_jit(kjit, p, b, 256, s) : launch_interp(p, b, 256, s); };
+    if (keyed_alloc(vm, n)) return fail(vm, XE_ERR_NOMEM, "device alloc (keyed execution)");
+    XeKeyed K = vm->kd;
+    if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, 128 * 4, s)) return fail(vm, XE_ERR_DEVICE, "keyed reset");
+    const uint32_t grid = parallel_grid(vm, kjit, general, n, P.nmaps);
+    XeParams X = P;
+    if (general && ensure_arena(vm, false, grid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+    // 1. SPEC: every packet against the start state, writes held back, keys logged
+    X.mode = XE_MODE_SPEC;
+    X.K = K;
+    if (klaunch(&X, grid) || fold()) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed spec)");
+    if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed spec)");
+    uint32_t flags = uint32_t(red[0]);
+    if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) return rollback(false) ? -1 : 1;
+    if (!(flags & XE_FLAG_KEYED)) {  // no packet wrote a map entry: an ordinary parallel run
+      if (run_conflict(red, P.nmaps)) return rollback(false) ? -1 : 1;
+      used_out = XE_MODE_PARALLEL;
+      return 0;
+    }
+    // 2. build: D, chains (union-find rounds), each packet's chain, the sorted order, chain starts
+    auto step = [&](uint32_t st, uint32_t items) { return launch_keyed(&K, vm->d_maps, vm->d_skip, st, items, s); };
+    uint32_t small[128];
+    auto read_small = [&]() { return d2h(small, vm->d_ksmall, sizeof small, s) || dsync(s); };
+    if (step(XE_KS_DSET, n)) return fail(vm, XE_ERR_DEVICE, "keyed build");
+    for (int round = 0;; round++) {
+      if (round >= 64) return rollback(false) ? -1 : 1;
+      if (dmemset(K.changed, 0, 4, s) || step(XE_KS_UNION, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
+      if (!small[65]) break;
+    }
+    if (step(XE_KS_COMPRESS, K.dcap) || step(XE_KS_ASSIGN, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
+    if (small[64] || small[68] > K.ins_cap) return rollback(false) ? -1 : 1;  // key log or insert log overflow
+    // a HASH insert can fail for capacity only in an order-dependent way: every key of D fits
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      HostMap& m = vm->maps[i];
+      if (m.dkind != XE_DM_HASH || i >= 64 || !small[i]) continue;
+      uint32_t cnt = 0;
+      if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+      if (uint64_t(cnt) + small[i] > m.def.max_entries) return rollback(false) ? -1 : 1;
+    }
+    const uint32_t nO = small[66];
+    uint32_t end_bit = 1;
+    while ((1ull << end_bit) <= K.dcap) end_bit++;
+    size_t sb = 0;
+    if (step(XE_KS_IOTA, n) || launch_keyed_sort(&K, n, end_bit, nullptr, &sb, s) ||
+        ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb) || launch_keyed_sort(&K, n, end_bit, vm->d_ksort, &sb, s))
+      return fail(vm, XE_ERR_DEVICE, "keyed sort");
+    K.nO = nO;
+    if (step(XE_KS_STARTS, nO) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
+    K.nchains = small[67];
+    // 3. back to the start state; reserve a slot record for every new HASH key of D
+    if (rollback(false) || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
+    if (step(XE_KS_RESERVE, small[68]) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");
+    if (small[64]) return rollback(true) ? -1 : 1;
+    // 4. the packets on no chain, in parallel
+    X.mode = XE_MODE_PARALLEL;
+    X.K = K;
+    X.K.skip = vm->d_skip;
+    if (nO < n && (klaunch(&X, grid) || fold())) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed parallel)");
+    // 5. the chains, one lane each, in packet order
+    X.mode = XE_MODE_CHAIN;
+    X.K.skip = nullptr;
+    const uint32_t cgrid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (K.nchains + 255) / 256));
+    if (klaunch(&X, cgrid)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
+    if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
+    if (run_conflict(red, P.nmaps)) return rollback(true) ? -1 : 1;  // a packet left its chain / an order-dependent add
+    vm->last_grid = grid;
+    used_out = XE_MODE_KEYED;
+    return 0;
+  };
+
   vm->t0.rec(s);
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
   float kms = 0;
+  const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && !has_ordered_maps(vm);
   if (mode == XE_MODE_SEQUENTIAL || (mode == XE_MODE_AUTO && has_ordered_maps(vm)) || overlap) {
     // ordered maps: every operation on them is order-dependent; replay straight away
     used = XE_MODE_SEQUENTIAL;
     if (int rc = sequential(kms)) return rc;
+  } else if (keyed_ok && vm->keyed_hint) {
+    // the last batch wrote map entries: straight to the keyed path
+    const int r = keyed(used);
+    if (r < 0) return r;
+    if (r == 1) {
+      vm->keyed_refused = true;
+      used = XE_MODE_SEQUENTIAL;
+      if (int rc = sequential(kms)) return rc;
+    }
+    conflict = used != XE_MODE_PARALLEL;
+    vm->t1.rec(s);
+    if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
+    kms += Timer::ms(vm->t0, vm->t1);
   } else {
     P.mode = XE_MODE_PARALLEL;
     vm->last_grid = parallel_grid(vm, jit, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
     vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
-    // fold the 8-byte-add replicas into the value regions (and zero them for the next run)
-    for (size_t i = 1; i < vm->maps.size(); i++) {
-      HostMap& m = vm->maps[i];
-      if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
-        return fail(vm, XE_ERR_DEVICE, "replica fold");
-    }
+    if (fold()) return fail(vm, XE_ERR_DEVICE, "replica fold");
     if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
     kms = Timer::ms(vm->t0, vm->t1);
     const uint32_t flags = uint32_t(red[0]);
     conflict = run_conflict(red, P.nmaps);
     if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
-      // order-dependent batch (or a lane out of arena): roll the maps back and replay in packet order
+      // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the
+      // keyed path, everything else (and what the keyed path refuses) the replay in packet order
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
-      used = XE_MODE_SEQUENTIAL;
-      if (int rc = sequential(kms)) return rc;
+      int r = 1;
+      if (keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY) && !vm->keyed_refused) {
+        vm->t2.rec(s);
+        r = keyed(used);
+        if (r < 0) return r;
+        vm->keyed_refused = r == 1;
+        if (r == 0) {
+          vm->t1.rec(s);
+          if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
+          kms += Timer::ms(vm->t2, vm->t1);
+        }
+      }
+      if (r == 1) {
+        used = XE_MODE_SEQUENTIAL;
+        if (int rc = sequential(kms)) return rc;
+      }
+    } else if (!conflict) {
+      vm->keyed_refused = false;
     }
   }
+  vm->keyed_hint = used == XE_MODE_KEYED;
+  if (used == XE_MODE_KEYED) red[0] |= XE_FLAG_ORDERED;  // order-dependent effects (shard checks replay it)
   record_widths(vm, red, P.nmaps);
-  if (used == XE_MODE_SEQUENTIAL) {
+  if (used == XE_MODE_SEQUENTIAL || used == XE_MODE_KEYED) {
     // in-program inserts change the entry count: refresh the replica-sizing hint
     std::vector<uint32_t> counts(vm->maps.size(), 0);
     for (size_t i = 1; i < vm->maps.size(); i++)
@@ -1789,7 +2023,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     stats->kernel_ms = kms;
     stats->total_ms = kms;
     stats->engine_used = jit ? XE_ENGINE_JIT : XE_ENGINE_INTERP;
-    stats->grid_blocks = used == XE_MODE_PARALLEL ? vm->last_grid : 1;
+    stats->grid_blocks = used == XE_MODE_SEQUENTIAL ? 1 : vm->last_grid;
   }
   return XE_OK;
 }
@@ -2143,7 +2377,7 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
   const std::vector<unsigned long long>& fp = ep ? vm->epoch_fp : vm->last_fp;
   uint64_t f = ep ? XE_FPF_EPOCH : 0;
   if (flags & XE_FLAG_ORDERED) f |= XE_FPF_ORDERED;
-  if (ep ? vm->epoch_seq : vm->last_mode == XE_MODE_SEQUENTIAL) f |= XE_FPF_SEQUENTIAL;
+  if (ep ? vm->epoch_seq : (vm->last_mode == XE_MODE_SEQUENTIAL || vm->last_mode == XE_MODE_KEYED)) f |= XE_FPF_SEQUENTIAL;
   if (flags & XE_FLAG_UNALIGNED) f |= XE_FPF_UNALIGNED;
   out[0] = f;
   for (uint32_t m = 1; m <= nm; m++) {

@@ -26,7 +26,7 @@ MAP_LRU_HASH, MAP_LRU_PERCPU_HASH, MAP_ARRAY_OF_MAPS, MAP_HASH_OF_MAPS, MAP_QUEU
 ARRAY_TYPES = (MAP_ARRAY, MAP_PERCPU_ARRAY, MAP_PROG_ARRAY, MAP_ARRAY_OF_MAPS)
 HASH_TYPES = (MAP_HASH, MAP_PERCPU_HASH, MAP_HASH_OF_MAPS, MAP_LRU_HASH, MAP_LRU_PERCPU_HASH)
 LIST_TYPES = (MAP_QUEUE, MAP_STACK, MAP_PERF_EVENT_ARRAY)
-MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL = 0, 1, 2
+MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL, MODE_KEYED = 0, 1, 2, 3  # MODE_KEYED: mode_used only
 ENGINE_AUTO, ENGINE_INTERP, ENGINE_JIT = 0, 1, 2
 
 

@@ -8,6 +8,8 @@ regenerates identical packets; seed_c = 0x6F62706C64000000 + c.
   C3  5-tuple -> HASH lookup -> REDIRECT + hit counter, IMIX 64/576/1500 B, 64K flows preloaded
   C4  ~200-insn JEQ/JGT ACL (48 rules) on 1500 B packets, lane-divergence stress
   C5  C2-style parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets, sharded
+  C3-learn  C3 with flow learning: a miss inserts the flow (bpf_map_update_elem) — map-entry writes,
+            order-dependent (the keyed path, xe_internal.h XE_MODE_SPEC / XE_MODE_CHAIN)
 
 All programs avoid JLT/JLE/JSET (rejected by emulator/inst.go Translate) and use only helper 1
 (map lookup) — bpf_redirect does not exist in the reference emulator, so REDIRECT is `r0 = 4`.
@@ -145,6 +147,43 @@ def prog_c3() -> list[int]:
     a.jmp(JEQ, 3, "pass", imm=0)
     a.mov64(0, XDP_REDIRECT)
     a.exit()
+    a.label("pass")
+    a.mov64(0, XDP_PASS)
+    a.exit()
+    return a.assemble()
+
+
+def prog_c3learn() -> list[int]:
+    """C3 with flow learning: hit -> hits += 1, REDIRECT; miss -> insert {flow_id = saddr | 1 << 32,
+    hits = 1} (bpf_map_update_elem, BPF_ANY), PASS. Later packets of a learned flow hit it."""
+    a = Asm()
+    _parse_eth(a, "pass")
+    a.jmp(JNE, 3, "pass", imm=0x0008)
+    a.mov64(2, src=6).add64(2, src=4)
+    a.mov64(5, src=2).add64(5, 24)
+    a.jmp(JGT, 5, "pass", src=7)
+    _tuple_key(a)
+    a.ld_map(1, 1)
+    a.mov64(2, src=10).add64(2, -16)
+    a.call(1)
+    a.jmp(JEQ, 0, "learn", imm=0)
+    a.mov64(1, 1)
+    a.xadd(8, 0, 8, 1)                      # value.hits += 1
+    a.ldx(8, 3, 0, 0)                       # flow_id
+    a.jmp(JEQ, 3, "pass", imm=0)
+    a.mov64(0, XDP_REDIRECT)
+    a.exit()
+    a.label("learn")
+    a.ldx(4, 3, 10, -16)                    # saddr from the key
+    a.mov64(4, 1).alu64(0x60, 4, 32)        # r4 = 1 << 32 (LSH)
+    a.alu64(0x40, 3, src=4)                 # flow_id = saddr | 1 << 32 (OR)
+    a.stx(8, 10, -32, 3)
+    a.st(8, 10, -24, 1)                     # hits = 1
+    a.ld_map(1, 1)
+    a.mov64(2, src=10).add64(2, -16)
+    a.mov64(3, src=10).add64(3, -32)
+    a.mov64(4, 0)                           # BPF_ANY
+    a.call(2)                               # bpf_map_update_elem
     a.label("pass")
     a.mov64(0, XDP_PASS)
     a.exit()
@@ -325,6 +364,7 @@ C3_FLOWS = 65536
 C3_MAX = 1 << 20
 C5_FLOWS = 1 << 20
 C5_MAX = 1 << 20
+C3_NEW_FLOWS = 1 << 18   # C3-learn: the flows misses come from (learned on first sight)
 
 
 def zipf_ranks(u: np.ndarray, nflows: int, s: float = 1.1) -> np.ndarray:
@@ -342,6 +382,17 @@ def headers_c3(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
     fid = zipf_ranks(u, C3_FLOWS).astype(np.uint64)
     miss_id = np.uint64(C3_FLOWS) + (rng_stream(3, idx, 3) % np.uint64(1 << 30))
     fid = np.where(hit, fid, miss_id)
+    return _ipv4_l4_headers(3, idx, flow_tuples(3, fid), hdr)
+
+
+def headers_c3learn(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
+    """C3's stream, its 10% misses drawn from C3_NEW_FLOWS flows that are not preloaded."""
+    r0 = rng_stream(3, idx, 0)
+    u = (r0 >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    hit = (rng_stream(3, idx, 2) % np.uint64(10)) != 0
+    fid = zipf_ranks(u, C3_FLOWS).astype(np.uint64)
+    new_id = np.uint64(C3_FLOWS) + (rng_stream(3, idx, 3) % np.uint64(C3_NEW_FLOWS))
+    fid = np.where(hit, fid, new_id)
     return _ipv4_l4_headers(3, idx, flow_tuples(3, fid), hdr)
 
 
@@ -398,6 +449,7 @@ CONFIGS = {
     "c2": dict(program=prog_c2, pkt=64, n=16 * 1024 * 1024),
     "c2rmw": dict(program=lambda: prog_c2(rmw=True), pkt=64, n=16 * 1024 * 1024),
     "c3": dict(program=prog_c3, pkt="imix", n=16 * 1024 * 1024),
+    "c3learn": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
     "c4": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024),
     "c5": dict(program=prog_c5, pkt=64, n=256 * 1024 * 1024),
 }
@@ -406,7 +458,7 @@ CONFIGS = {
 def workload_maps(name: str) -> list[tuple[MapDef, tuple[np.ndarray, np.ndarray] | None]]:
     if name in ("c2", "c2rmw"):
         return [(MapDef(MAP_ARRAY, 4, 8, 256), None)]
-    if name == "c3":
+    if name in ("c3", "c3learn"):
         return [(MapDef(MAP_HASH, 16, 16, C3_MAX), c3_map_entries())]
     if name == "c5":
         return [(MapDef(MAP_HASH, 16, 16, C5_MAX), c5_map_entries())]
@@ -420,7 +472,8 @@ def headers(name: str, idx: np.ndarray, hdr: int = 64) -> np.ndarray:
         for b in range(hdr):
             h[:, b] = (r >> np.uint64(8 * (b % 8))) & np.uint64(0xFF)
         return h
-    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c4": headers_c4, "c5": headers_c5}[name](idx, hdr)
+    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c4": headers_c4,
+            "c5": headers_c5}[name](idx, hdr)
 
 
 def packet_sizes(name: str, idx: np.ndarray) -> np.ndarray:

@@ -123,6 +123,7 @@ extern "C" {
 #define XE_MODE_AUTO 0       /* parallel, verified; falls back to ordered device execution on conflict */
 #define XE_MODE_PARALLEL 1   /* parallel only; conflicts reported in stats, results kept            */
 #define XE_MODE_SEQUENTIAL 2 /* exact packet order on one device lane                             */
+#define XE_MODE_KEYED 3      /* (xe_batch_stats.mode_used only) map-entry writes: per-key chains  */
 
 /* AF_XDP descriptor, exactly the layout of gobpfld's xsk.go:695-701 */
 typedef struct xe_desc {
@@ -175,7 +176,7 @@ typedef struct xe_batch_stats {
     uint64_t packets;
     uint64_t steps;            /* instructions retired over the batch */
     uint64_t status_count[8];  /* histogram of xe_result.status */
-    uint32_t mode_used;        /* XE_MODE_PARALLEL or XE_MODE_SEQUENTIAL */
+    uint32_t mode_used;        /* XE_MODE_PARALLEL, XE_MODE_KEYED or XE_MODE_SEQUENTIAL */
     uint32_t conflict;         /* 1 if the parallel run was order-dependent */
     float kernel_ms;           /* device time of the interpreter launch(es) */
     float total_ms;            /* device time of the whole call */

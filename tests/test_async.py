@@ -11,7 +11,7 @@ import pytest
 
 from gobpfld_amd import workloads as W
 from gobpfld_amd.asm import JNE, Asm
-from gobpfld_amd.emulator import MAP_ARRAY, MODE_PARALLEL, MODE_SEQUENTIAL, VM, MapDef, Settings
+from gobpfld_amd.emulator import MAP_ARRAY, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, VM, MapDef, Settings
 from parity import packets
 
 MARK = 0xEE
@@ -90,7 +90,8 @@ def test_async_stream_equals_oracle_hostsim(hostsim_lib, oracle_lib, marked, ent
     for b in range(len(bs)):
         assert (ver_a[b] == ver_o[b]).all() and (ver_s[b] == ver_o[b]).all(), f"batch {b}"
         want_seq = b in marked
-        assert st_a[b]["mode_used"] == (MODE_SEQUENTIAL if want_seq else MODE_PARALLEL), (b, st_a[b])
+        # the marked store writes one map entry: keyed ordered execution (its key's chain in order)
+        assert st_a[b]["mode_used"] == (MODE_KEYED if want_seq else MODE_PARALLEL), (b, st_a[b])
         assert st_a[b]["conflict"] == int(want_seq)
         assert st_a[b]["status_count"] == st_s[b]["status_count"] and st_a[b]["steps"] == st_s[b]["steps"]
 
@@ -185,7 +186,7 @@ def test_async_stream_equals_oracle_gpu(gpu_lib, oracle_lib, marked, entries):
     assert vm.map_dump(m) == dump_o
     for b, (_, _, dv) in enumerate(dev):
         assert (dv.cpu().numpy().view(np.uint32) == ver_o[b]).all(), f"batch {b}"
-        assert sts[b]["mode_used"] == (MODE_SEQUENTIAL if b in marked else MODE_PARALLEL), (b, sts[b])
+        assert sts[b]["mode_used"] == (MODE_KEYED if b in marked else MODE_PARALLEL), (b, sts[b])
     vm.close()
 
 

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from gobpfld_amd import workloads as W
-from gobpfld_amd.emulator import EmulatorError, ENGINE_INTERP, ENGINE_JIT, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
+from gobpfld_amd.emulator import EmulatorError, ENGINE_INTERP, ENGINE_JIT, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
 from kats import KATS
 from parity import assert_same, config_case, packets, run_one
 
@@ -60,7 +60,8 @@ def test_ordered_program_falls_back(gpu_lib, oracle_lib, engine):
     a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, settings=Settings(engine=engine))
     b = run_one(oracle_lib, k["program"], k["maps"], umem, descs)
     assert_same(a, b, "ordered rmw")
-    assert a[0].stats["conflict"] == 1 and a[0].stats["mode_used"] == MODE_SEQUENTIAL
+    # one key written by every packet: a single chain (keyed ordered execution), in packet order
+    assert a[0].stats["conflict"] == 1 and a[0].stats["mode_used"] == MODE_KEYED
     # packet i saw counter value i: the exact sequential order
     assert (a[0].results["r0"] == np.arange(3000)).all()
 

@@ -15,6 +15,7 @@ def prod(built):
     lib = C.CDLL(str(PRODUCT_LIB))
     lib.xe_translate_uops.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
     lib.xe_jit_compile_check.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    lib.xe_jit_compile_check_keyed.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
     lib.xe_jit_source.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
     return lib
 
@@ -32,6 +33,14 @@ def test_config_kernel_compiles(prod, name):
     u, n = _uops(prod, W.CONFIGS[name]["program"]())
     log = C.create_string_buffer(4096)
     assert prod.xe_jit_compile_check(u.ctypes.data, n, log, 4096) == 0, log.value.decode()
+
+
+@pytest.mark.parametrize("name", ["c2rmw", "c3learn", "c5"])
+def test_keyed_variant_compiles(prod, name):
+    """The keyed variant (XE_MODE_SPEC / XE_MODE_CHAIN, xe_internal.h) of the per-program kernel."""
+    u, n = _uops(prod, W.CONFIGS[name]["program"]())
+    log = C.create_string_buffer(4096)
+    assert prod.xe_jit_compile_check_keyed(u.ctypes.data, n, log, 4096) == 0, log.value.decode()
 
 
 def test_kat_kernels_compile(prod):

@@ -12,7 +12,7 @@ import pytest
 
 from gobpfld_amd import workloads as W
 from gobpfld_amd.asm import ADD, JEQ, MUL, Asm
-from gobpfld_amd.emulator import MAP_ARRAY, MODE_PARALLEL, MODE_SEQUENTIAL, MapDef, Settings
+from gobpfld_amd.emulator import MAP_ARRAY, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, MapDef, Settings
 from parity import assert_same, config_case, packets, run_one
 
 UF_LIFT = 0x40
@@ -59,6 +59,15 @@ def _prog(variant):
 
 LIFTED = ["add_imm64", "sub_reg64", "add32_reg_w4", "two_fields"]
 ORDERED = ["used_after", "other_read", "mul"]
+
+
+def _mode(variant, parallel, regs=False):
+    """Lifted: parallel. A plain store into the value (not lifted): keyed ordered execution (chains per
+    written key). other_read, lifted (no register records): a plain read of a field other lanes add to,
+    the one-lane replay."""
+    if parallel:
+        return MODE_PARALLEL
+    return MODE_SEQUENTIAL if variant == "other_read" and not regs else MODE_KEYED
 
 
 def test_lift_static_pattern():
@@ -113,7 +122,7 @@ def test_lift_hostsim_equals_oracle(oracle_lib, hostsim_lib, variant, regs):
     b = run_one(oracle_lib, _prog(variant), _maps(), umem, descs, regs=regs)
     assert_same(a, b, variant)
     parallel = variant in LIFTED and not regs
-    assert a[0].stats["mode_used"] == (MODE_PARALLEL if parallel else MODE_SEQUENTIAL), variant
+    assert a[0].stats["mode_used"] == _mode(variant, parallel, regs), variant
     assert a[0].stats["conflict"] == (0 if parallel else 1), variant
 
 
@@ -135,8 +144,7 @@ def test_lift_device_equals_oracle(gpu_lib, oracle_lib, variant, engine):
     a = run_one(gpu_lib, _prog(variant), _maps(), umem, descs, regs=False, settings=Settings(engine=engine))
     b = run_one(oracle_lib, _prog(variant), _maps(), umem, descs, regs=False)
     assert_same(a, b, variant)
-    parallel = variant in LIFTED
-    assert a[0].stats["mode_used"] == (MODE_PARALLEL if parallel else MODE_SEQUENTIAL), variant
+    assert a[0].stats["mode_used"] == _mode(variant, variant in LIFTED), variant
 
 
 @pytest.mark.gpu

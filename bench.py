@@ -33,6 +33,8 @@ WORKLOADS = {
     "c3": "C3: 5-tuple HASH lookup -> REDIRECT + hit counter, 64K flows, IMIX 64/576/1500 B",
     "c4": "C4: ~200-insn JEQ/JGT ACL (48 rules), 1500 B packets, lane-divergence stress",
     "c5": "C5: C2 parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets",
+    "c3learn": "C3-learn: C3 whose misses (10%, 262,144 new flows) insert the flow (bpf_map_update_elem, BPF_ANY): "
+               "map-entry writes, order-dependent; IMIX 64/576/1500 B",
     "c2rmw": "C2-RMW: C2 with the per-proto counter bumped by a plain load/add/store (value->packets++ without "
              "an atomic): the ordered read-modify-write, run in parallel through lift_rmw",
 }  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec peak
@@ -197,6 +199,46 @@ def ordered_paths(d_umem, d_desc, n: int, dev, stream, seq_sample: int = 65536) 
     return out
 
 
+def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536) -> dict:
+    """C3-learn (C3 with flow learning: a miss inserts the flow with bpf_map_update_elem) on fresh map
+    state each run: the keyed ordered execution over all n packets (SPEC pass, chains per written key,
+    xe_internal.h) and, for scale, the one-lane in-order replay (MODE_SEQUENTIAL) on the first
+    `seq_sample` packets. Map upload and kernel compilation stay outside the timed region (a 0-packet
+    run first); the first run of each path is a warm-up."""
+    import torch
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import MODE_SEQUENTIAL, VM, Settings
+    umem, descs = W.build_batch("c3learn", 0, n)
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
+    d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    del umem
+    out = {"program": WORKLOADS["c3learn"]}
+    for key, mode, cnt, r in (("keyed", 0, n, reps), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
+        times, ks, modes, grids = [], [], set(), 0
+        for k in range(r + 1):
+            vm = VM(Settings(device=dev.index or 0, mode=mode))
+            W.setup_vm(vm, "c3learn")
+            vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), 0, stream=stream)  # upload
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), cnt,
+                                     d_verdicts=d_ver.data_ptr(), stream=stream)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            if k:
+                times.append(dt)
+                ks.append(st["kernel_ms"])
+                modes.add(st["mode_used"])
+                grids = st["grid_blocks"]
+            vm.close()
+        dt = float(np.median(times))
+        out[key] = {"value": round(cnt / dt / 1e6, 3), "unit": "Mpkt/s", "packets": cnt, "ms_per_batch": round(dt * 1e3, 3),
+                    "device_ms": round(float(np.median(ks)), 3), "mode_used": sorted(modes), "grid_blocks": grids,
+                    "runs": len(times)}
+    return out
+
+
 def single_process_multi(args, name: str, n: int) -> None:
     """`bench.py --gpus N` without torchrun: one process drives N GPUs through the C ABI
     (xe_multi_create / xe_run_batch_multi: concurrent shards, RCCL delta all-reduce or in-order
@@ -266,6 +308,8 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     ap.add_argument("--no-ordered", action="store_true", help="skip the C2-RMW ordered-path lines (C2 only)")
     ap.add_argument("--sync", action="store_true", help="one synchronous xe_run_batch_device per step (no pipelining)")
+    ap.add_argument("--keyed-packets", type=int, default=4 * 1024 * 1024,
+                    help="C3-learn batch of the keyed ordered-execution line (C2 runs only)")
     args = ap.parse_args()
 
     import torch
@@ -377,6 +421,7 @@ def main() -> None:
     ordered = None
     if rank == 0 and name == "c2" and not args.no_ordered:
         ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
+        ordered["keyed_c3learn"] = keyed_paths(dev, stream, args.keyed_packets)
     del umem
     if rank == 0:
         cpu = None

@@ -2096,7 +2096,8 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   const bool entry_ok = vm->entry >= 1 && vm->entry < int32_t(vm->programs.size());
   // batches that cannot pipeline run synchronously, after everything in flight
-  if (!entry_ok || vm->settings.mode == XE_MODE_SEQUENTIAL || has_ordered_maps(vm) ||
+  // (keyed_hint: the last batch wrote map entries, this one starts with the keyed path's SPEC pass)
+  if (!entry_ok || vm->settings.mode == XE_MODE_SEQUENTIAL || has_ordered_maps(vm) || vm->keyed_hint ||
       (umem_len && may_write_packet(vm->programs[vm->entry])))
     return xe_run_batch_device(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, stream, stats);
   if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");

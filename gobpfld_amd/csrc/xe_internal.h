@@ -194,10 +194,11 @@ XE_HD uint64_t xe_hash_words(const uint64_t* w, uint32_t nwords, uint32_t key_si
 #define XE_MODE_CHAIN 17u
 #define XE_KLOG 4u            // keys a packet may touch (more: the batch takes the one-lane replay)
 #define XE_SLOT_BUSY 8u       // a slot record being reserved (key words not yet written)
-#define XE_INS_WORDS 9u       // insert-log entry: map index, then the zero-padded key words
+#define XE_SLOT_NEW 16u       // a tombstone reserved by the current reservation launch
 
-// key id of map m's key: 6 bits of map index, 56 bits of a mixed key hash, bit 1 set (never 0), bit 0
-// clear (the key log uses it as the "written" mark)
+// key id of map m's key: 6 bits of map index, 54 bits of a mixed key hash, low nibble 0b0010 (never 0;
+// the key log uses bit 0 as the "written" mark, bit 2 "an insert whose key words are in ikey slot
+// bit 3")
 XE_HD uint64_t xe_kid_mix(uint64_t x) {
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
@@ -207,33 +208,51 @@ XE_HD uint64_t xe_kid_mix(uint64_t x) {
   return x;
 }
 XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
-  return (uint64_t(m & 63u) << 58) | (xe_kid_mix(h) & ((1ull << 58) - 4ull)) | 2ull;
+  return (uint64_t(m & 63u) << 58) | (xe_kid_mix(h) & ((1ull << 58) - 16ull)) | 2ull;
 }
+#define XE_KLOG_W 1ull        // key log entry: the key is written
+#define XE_KLOG_INS 4ull      // ... by an insert whose key words are in the packet's ikey slot (bit 3)
+#define XE_KLOG_FLAGS 0xDull
+#define XE_KINS 2u            // ikey slots per packet (more held-back inserts: the one-lane replay)
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
-enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_STARTS, XE_KS_RESERVE };
+enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
+                  XE_KS_COUNT };
+// Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
+// a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
+// a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
+// Small-buffer layout (u32 words):
+#define XE_KSTRIPES 32
+#define XE_KS_DCOUNT 0                      // [64 maps] D keys per map
+#define XE_KS_ERR 64                        // build errors
+#define XE_KS_CHANGED 65                    // union-find round changed something
+#define XE_KS_NO 66                         // packets on chains
+#define XE_KS_CINS 128                      // [64 maps][XE_KSTRIPES] inserts the chains made
+#define XE_KS_WORDS (128 + 64 * XE_KSTRIPES)
+#define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid
 #define XE_KID_ARRAY_TAG 0xA7A7A7A700000000ull
 #define XE_KID_NIL_KEY 0x6e696c6b65790001ull  // the nil (empty) hash key
 
 struct XeKeyed {
   uint64_t* klog;      // [n * XE_KLOG] key ids a packet touched (| 1: written)
   uint32_t* kcnt;      // [n] keys the packet touched (> XE_KLOG: overflow)
-  uint64_t* ins;       // insert log: [ins_cap * XE_INS_WORDS], entries of held-back HASH inserts
-  uint32_t* nins;      // entries appended
-  uint32_t ins_cap;
   uint32_t dcap;       // D table slots (power of two)
+  uint32_t kw;         // words of a dkey entry: 1 + the longest HASH key's words
   uint64_t* dkid;      // D table: key ids (0 = free)
   uint32_t* dcomp;     // D table: chain (union-find parent, then the root)
-  uint32_t* drep;      // D table: the insert-log entry that reserves the key (XE_NONE: none yet)
+  uint64_t* dkey;      // D table: [dcap * kw] a held-back insert's key (word 0: map | 0x100 nil | VALID)
+  uint64_t* ikey;      // [n * XE_KINS * kw] the key words of a packet's held-back inserts (SPEC)
   uint32_t* dcount;    // [64] D keys per map (HASH capacity bound)
-  uint32_t* err;       // build errors: 1 = key log overflow, 2 = no slot for a reservation, 4 = insert without D key
+  uint32_t* cins;      // [64][XE_KSTRIPES] inserts made by the chains (added to the map counts after)
+  uint32_t* err;       // build errors: 1 key log overflow, 2 no slot for a reservation, 8 D full
   uint32_t* changed;   // union-find round changed something
   uint32_t* ckey;      // [n] chain of packet i (dcap: none)
   uint32_t* okey;      // [n] sorted chain keys
   uint32_t* order;     // [n] packet indices sorted by chain, in packet order within a chain
-  uint32_t* cbeg;      // [n] start of each chain in order[]
-  uint32_t* counts;    // [0] packets on chains, [1] chains
+  uint32_t* iota;      // [n] 0..n-1 (sort input)
+  uint32_t* counts;    // [0] packets on chains (nO)
   const uint8_t* skip; // [n] 1 = the packet runs on a chain (the parallel pass leaves it out)
-  uint32_t nO, nchains;
+  uint32_t n;          // packets of the batch
+  uint32_t nO;         // packets on chains: order[0..nO) (a chain starts where the sorted key changes)
 };
 
 // General lane model (xe_interp.h, XE_GEN): the Go object model without fixed limits, per lane in a

@@ -80,12 +80,11 @@ XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long l
 XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
   return __hip_atomic_fetch_min((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-XE_DEV unsigned long long xe_load_acquire64(unsigned long long* p) {
-  return __hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+XE_DEV unsigned long long xe_load_relaxed64(unsigned long long* p) {
+  return __hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-XE_DEV void xe_store_release64(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store((XE_GP(unsigned long long))p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
+XE_DEV uint64_t xe_lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
+XE_DEV uint32_t xe_shfl32(uint32_t v, int l) { return uint32_t(__shfl(int(v), l)); }
 #else
 #define XE_DEV static inline
 #define XE_WAVE 1
@@ -116,9 +115,52 @@ XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
   while (v < o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
   return o;
 }
-XE_DEV unsigned long long xe_load_acquire64(unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
-XE_DEV void xe_store_release64(unsigned long long* p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+XE_DEV unsigned long long xe_load_relaxed64(unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+XE_DEV uint64_t xe_lanemask_lt() { return 0; }
+XE_DEV uint32_t xe_shfl32(uint32_t v, int) { return v; }
 #endif
+
+// Wave-aggregated counters: same-address atomics serialise at the memory side, so the lanes of a wave
+// that bump one counter do it with one atomic. Call with every active lane (want: this lane counts).
+// Returns this lane's index among the wave's counting lanes (offset from the old counter value).
+XE_DEV uint32_t xe_wave_alloc(unsigned int* counter, bool want) {
+  const uint64_t m = xe_ballot(want);
+  if (!m) return 0;
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (xe_lane() == leader) base = xe_atomic_add32(counter, uint32_t(__builtin_popcountll(m)));
+  base = xe_shfl32(base, leader);
+  return base + uint32_t(__builtin_popcountll(m & xe_lanemask_lt()));
+}
+// the same with a counter per lane: lanes grouped by counter address, one atomic per address per wave
+XE_DEV uint32_t xe_wave_alloc_at(unsigned int* p, bool want) {
+  uint64_t m = xe_ballot(want);
+  const uint64_t a = uint64_t(uintptr_t(p));
+  uint32_t mine = 0;
+  while (m) {
+    const int leader = __builtin_ctzll(m);
+    const uint64_t la = uint64_t(xe_shfl32(uint32_t(a), leader)) | (uint64_t(xe_shfl32(uint32_t(a >> 32), leader)) << 32);
+    const uint64_t same = m & xe_ballot(a == la);
+    uint32_t base = 0;
+    if (xe_lane() == leader) base = xe_atomic_add32(p, uint32_t(__builtin_popcountll(same)));
+    base = xe_shfl32(base, leader);
+    if ((same >> xe_lane()) & 1ull) mine = base + uint32_t(__builtin_popcountll(same & xe_lanemask_lt()));
+    m &= ~same;
+  }
+  return mine;
+}
+// *p += 1 for every lane with want, lanes grouped by counter address (one atomic per address per wave)
+XE_DEV void xe_wave_count(unsigned int* p, bool want) {
+  uint64_t m = xe_ballot(want);
+  const uint64_t a = uint64_t(uintptr_t(p));
+  while (m) {
+    const int leader = __builtin_ctzll(m);
+    const uint64_t la = uint64_t(xe_shfl32(uint32_t(a), leader)) | (uint64_t(xe_shfl32(uint32_t(a >> 32), leader)) << 32);
+    const uint64_t same = m & xe_ballot(a == la);
+    if (xe_lane() == leader) xe_atomic_add32(p, uint32_t(__builtin_popcountll(same)));
+    m &= ~same;
+  }
+}
 
 #if defined(XE_MEM_FIELDS)
 #define XE_GEN 0
@@ -343,8 +385,13 @@ struct XeLane {
   // (XE_MODE_CHAIN)
   uint64_t klog[XE_KLOG];
   uint32_t kn;
+  uint32_t kpkt;  // the packet's index (its ikey slots)
+  uint32_t kins;  // held-back inserts of the packet so far
   bool kwr;
+  bool kany;  // some packet of this wave held a write back (XE_FLAG_KEYED at the wave's flush)
   uint32_t kchain;
+  uint32_t kh;  // the last HASH value handle a lookup returned and its key id (value accesses through
+  uint64_t kk;  // it need not re-read the slot's key words)
 #endif
 };
 
@@ -771,7 +818,7 @@ XE_DEV uint64_t kid_slot(uint32_t m, const XeDevMap& M, uint32_t slot) {
 
 // D table (the keys some packet writes): open addressing over key ids, 0 = free
 XE_DEV int64_t dset_find(const XeKeyed& K, uint64_t kid) {
-  uint32_t idx = uint32_t(kid >> 2) & (K.dcap - 1);
+  uint32_t idx = uint32_t(kid >> 4) & (K.dcap - 1);
 #pragma unroll 1
   for (uint32_t p = 0; p < K.dcap; p++) {
     const uint64_t k = ((XE_GP(const uint64_t))K.dkid)[idx];
@@ -782,7 +829,7 @@ XE_DEV int64_t dset_find(const XeKeyed& K, uint64_t kid) {
   return -1;
 }
 
-XE_DEV bool keyed_dset_insert(const XeKeyed& K, uint64_t kid);
+XE_DEV int64_t keyed_dset_insert(const XeKeyed& K, uint64_t kid);
 
 // A map key the lane's packet touches (read / add: write = false; an ARRAY / HASH write: true).
 // SPEC: log it (repeats fold into one entry). CHAIN: a key of D must belong to the lane's chain, a
@@ -795,9 +842,9 @@ XE_DEV int key_touch(XeLane& L, const XeParams& P, uint64_t kid, bool write, boo
     bool found = false;
 #pragma unroll
     for (uint32_t j = 0; j < XE_KLOG; j++) {
-      if (j < L.kn && (L.klog[j] & ~1ull) == kid) {
+      if (j < L.kn && (L.klog[j] & ~XE_KLOG_FLAGS) == kid) {
         found = true;
-        if (write) L.klog[j] |= 1ull;
+        if (write) L.klog[j] |= XE_KLOG_W;
       }
     }
     if (!found) {
@@ -905,7 +952,7 @@ XE_DEV int key_touch_mem(XeLane& L, const XeParams& P, uint32_t h, const XeBMem&
   const XeDevMap M = map_desc(L, B.map);
   if (B.array) return key_touch_array(L, P, B.map, M, off, size, write, dkey);
   if (M.kind != XE_DM_HASH) return 0;  // the ordered maps never run keyed
-  return key_touch(L, P, kid_slot(B.map, M, xe_h_slot(h)), write, dkey);
+  return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, xe_h_slot(h)), write, dkey);
 }
 #endif
 
@@ -1497,11 +1544,12 @@ XE_DEV int64_t hash_insert_new(const XeDevMap& M, const uint64_t* kw, bool empty
 #if XE_KEYED
 // XE_MODE_CHAIN insert of an absent key: it takes the record reserved for it before the chains ran
 // (xe_keyed_reserve: a tombstone holding the key words), so no two lanes ever claim slots. -1: the
-// key has no reservation (its chain left the schedule).
-XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty) {
+// key has no reservation (its chain left the schedule). The entry count goes to the striped counter
+// cnt (folded into the map's count after the chains; no insert of a chain can hit the capacity).
+XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty, unsigned int* cnt) {
   if (empty) {
     hash_set_state(M, M.cap, XE_SLOT_FULL);
-    xe_atomic_add32(M.count, 1);
+    xe_wave_count(cnt, true);
     return int64_t(M.cap);
   }
   const uint32_t mask = M.cap - 1;
@@ -1516,7 +1564,7 @@ XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty) {
       for (uint32_t k = 0; k < M.kwords; k++) eq = eq && r[1 + k] == kw[k];
       if (eq) {
         r[0] = XE_SLOT_FULL;
-        xe_atomic_add32(M.count, 1);
+        xe_wave_count(cnt, true);
         return int64_t(idx);
       }
     }
@@ -1527,23 +1575,25 @@ XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty) {
 
 // Reserve a record for HASH key kw of map M (one lane per distinct key; the keyed build): the key's
 // present or earlier reserved record, else the first free slot of its chain, claimed BUSY by CAS,
-// then the key words, then the tombstone state. Returns false when the table has no free slot.
+// then the key words, then the tombstone state marked NEW. Records claimed in this launch (BUSY, NEW)
+// hold other keys (each key has one reserving lane) and are passed without reading their key words,
+// so no load needs acquire ordering. Returns false when the table has no free slot.
 XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw) {
   const uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(xe_hash_words(kw, M.kwords, M.key_size)) & mask;
 #pragma unroll 1
   for (uint32_t probe = 0; probe < M.cap;) {
     unsigned long long* r = reinterpret_cast<unsigned long long*>(M.keys + uint64_t(idx) * M.rwords);
-    const unsigned long long w0 = xe_load_acquire64(r);
+    const unsigned long long w0 = xe_load_relaxed64(r);
     const uint32_t st = uint32_t(w0);
-    if (st & (XE_SLOT_FULL | XE_SLOT_TOMB)) {
+    if ((st & (XE_SLOT_FULL | XE_SLOT_TOMB)) && !(st & XE_SLOT_NEW)) {
       bool eq = true;
       for (uint32_t k = 0; k < M.kwords; k++) eq = eq && ((XE_GP(const uint64_t))r)[1 + k] == kw[k];
       if (eq) return true;
-    } else if (!(st & XE_SLOT_BUSY)) {
+    } else if (!(st & (XE_SLOT_BUSY | XE_SLOT_NEW | XE_SLOT_FULL | XE_SLOT_TOMB))) {
       if (xe_atomic_cas64(r, w0, XE_SLOT_BUSY) != w0) continue;  // lost the slot: look at it again
       for (uint32_t k = 0; k < M.kwords; k++) ((XE_GP(uint64_t))r)[1 + k] = kw[k];
-      xe_store_release64(r, XE_SLOT_TOMB);
+      ((XE_GP(uint64_t))r)[0] = XE_SLOT_TOMB | XE_SLOT_NEW;
       return true;
     }
     idx = (idx + 1) & mask;
@@ -1690,8 +1740,11 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
     bool empty = false;
     if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2)) return e;
 #if XE_KEYED
-    if (M.kind == XE_DM_HASH)  // the key's presence is read
-      if (int e = key_touch(L, P, kid_hash(m, M, kw, empty), false)) return e;
+    uint64_t kid = 0;
+    if (M.kind == XE_DM_HASH && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)) {  // the key's presence is read
+      kid = kid_hash(m, M, kw, empty);
+      if (int e = key_touch(L, P, kid, false)) return e;
+    }
 #endif
 #if XE_HAS_ORDERED
     if (M.kind == XE_DM_LRU) {
@@ -1705,6 +1758,9 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
 #endif
     int64_t slot = hash_find(M, kw, empty);
     if (slot >= 0) out = XeReg{0, xe_h_make(XE_H_HASH, m, uint32_t(slot)), XE_KIND_MEMPTR};
+#if XE_KEYED
+    if (slot >= 0 && kid) { L.kh = out.h; L.kk = kid; }
+#endif
     return 0;
   }
 #if XE_HAS_ORDERED
@@ -1810,19 +1866,26 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
 #if XE_KEYED
     if (int e = key_touch(L, P, kid, true)) return e;
     if (P.mode == XE_MODE_SPEC) {  // held back; a new key goes to the insert log (its slot is reserved)
-      if (slot < 0 && keyed_dset_insert(P.K, kid)) {  // the first packet to insert the key logs it
-        const uint32_t at = xe_atomic_add32(P.K.nins, 1u);
-        if (at < P.K.ins_cap) {
-          XE_GP(uint64_t) en = (XE_GP(uint64_t))P.K.ins + uint64_t(at) * XE_INS_WORDS;
-          en[0] = uint64_t(m) | (empty ? 0x100ull : 0ull);
+      // a new key: its words go to the packet's next ikey slot (the build reserves its slot record)
+      if (slot < 0) {
+        if (L.kins >= XE_KINS) {
+          L.kn = XE_KLOG + 1;  // more inserts than slots: reported as a key-log overflow
+        } else {
+          XE_GP(uint64_t) en = (XE_GP(uint64_t))P.K.ikey + (uint64_t(L.kpkt) * XE_KINS + L.kins) * P.K.kw;
 #pragma unroll
-          for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) en[1 + w] = kw[w];
+          for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++)  // constant trip count: kw stays in registers
+            if (w + 1 < P.K.kw) en[1 + w] = kw[w];
+          en[0] = uint64_t(m) | (empty ? 0x100ull : 0ull) | XE_KEY_VALID;
+#pragma unroll
+          for (uint32_t j = 0; j < XE_KLOG; j++)
+            if (j < L.kn && (L.klog[j] & ~XE_KLOG_FLAGS) == kid) L.klog[j] |= XE_KLOG_INS | (uint64_t(L.kins) << 3);
+          L.kins++;
         }
       }
       return helper_errno_result(L, 0);
     }
     if (slot < 0 && P.mode == XE_MODE_CHAIN) {
-      slot = hash_claim(M, kw, empty);
+      slot = hash_claim(M, kw, empty, P.K.cins + m * XE_KSTRIPES + (L.wave % XE_KSTRIPES));
       if (slot < 0) return XE_EV_ORD;
     }
 #endif
@@ -2625,18 +2688,20 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
 // body(i, valid) runs the staged packet and calls lane_finish; all lanes call it together.
 // packet i runs in this parallel pass (the keyed path's pass leaves out the packets on chains)
 XE_DEV bool pkt_in_pass(const XeParams& P, uint32_t i) {
-#if XE_KEYED
   if (P.K.skip && i < P.n && ((XE_GP(const uint8_t))P.K.skip)[i]) return false;
-#endif
   return i < P.n;
 }
 // the key log of the lane's next packet starts empty
-XE_DEV void key_begin(XeLane& L) {
+XE_DEV void key_begin(XeLane& L, uint32_t i) {
 #if XE_KEYED
   L.kn = 0;
+  L.kpkt = i;
+  L.kins = 0;
   L.kwr = false;
+  L.kh = XE_NONE;
 #else
   (void)L;
+  (void)i;
 #endif
 }
 
@@ -2676,7 +2741,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     desc_load(P, i2, v2, r1lo, r1hi);
     const uint32_t abort_flags = xe_load_relaxed32(P.flags);
     lane_commit(L, P);  // the previous chunk's verdicts and adds, behind this chunk's prefetch
-    key_begin(L);
+    key_begin(L, i0);
     body(i0, v0);
     if (c1 >= nchunks) break;
     // a lane elsewhere needed an ordered write: this run will be discarded, stop early
@@ -2696,27 +2761,31 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
 // touches (rounds until nothing changes), the roots, each packet's chain (dcap: none), the chain
 // starts in the sorted order, and one slot reservation per new HASH key.
 // put key id `kid` into D; true when this call added it
-XE_DEV bool keyed_dset_insert(const XeKeyed& K, uint64_t kid) {
+// put key id `kid` into D; returns its slot when this call added it, else -1
+XE_DEV int64_t keyed_dset_insert(const XeKeyed& K, uint64_t kid) {
   const uint32_t mask = K.dcap - 1;
-  uint32_t idx = uint32_t(kid >> 2) & mask;
+  uint32_t idx = uint32_t(kid >> 4) & mask;
+  int64_t added = -1;
+  bool done = false;
 #pragma unroll 1
-  for (uint32_t probe = 0; probe < K.dcap; probe++) {
-    const unsigned long long cur = xe_load_acquire64(reinterpret_cast<unsigned long long*>(K.dkid + idx));
-    if (cur == kid) return false;
+  for (uint32_t probe = 0; probe < K.dcap && !done; probe++) {
+    const unsigned long long cur = xe_load_relaxed64(reinterpret_cast<unsigned long long*>(K.dkid + idx));
+    if (cur == kid) { done = true; break; }
     if (cur == 0) {
       const unsigned long long old = xe_atomic_cas64(reinterpret_cast<unsigned long long*>(K.dkid + idx), 0ull, kid);
       if (old == 0) {
         K.dcomp[idx] = idx;
-        K.drep[idx] = XE_NONE;
-        xe_atomic_add32(K.dcount + (kid >> 58), 1u);
-        return true;
+        K.dkey[uint64_t(idx) * K.kw] = 0;  // no key words (yet): not an insert
+        added = int64_t(idx);
+        done = true;
+        break;
       }
-      if (old == kid) return false;
+      if (old == kid) { done = true; break; }
     }
     idx = (idx + 1) & mask;
   }
-  xe_atomic_or32(K.err, 8u);  // D is full
-  return false;
+  if (!done) xe_atomic_or32(K.err, 8u);  // D is full
+  return added;
 }
 XE_DEV void keyed_dset_item(const XeKeyed& K, uint32_t i) {
   const uint32_t n = K.kcnt[i];
@@ -2724,7 +2793,13 @@ XE_DEV void keyed_dset_item(const XeKeyed& K, uint32_t i) {
 #pragma unroll 1
   for (uint32_t j = 0; j < n; j++) {
     const uint64_t e = K.klog[uint64_t(i) * XE_KLOG + j];
-    if (e & 1ull) keyed_dset_insert(K, e & ~1ull);
+    if (!(e & XE_KLOG_W)) continue;
+    const int64_t d = keyed_dset_insert(K, e & ~XE_KLOG_FLAGS);
+    if (d >= 0 && (e & XE_KLOG_INS)) {  // the key's first writer: an insert, its words go with the D slot
+      const uint64_t* src = K.ikey + (uint64_t(i) * XE_KINS + ((e >> 3) & 1ull)) * K.kw;
+      uint64_t* dst = K.dkey + uint64_t(d) * K.kw;
+      for (uint32_t w = 0; w < K.kw; w++) dst[w] = src[w];
+    }
   }
 }
 XE_DEV uint32_t keyed_root(const XeKeyed& K, uint32_t x) {
@@ -2742,13 +2817,13 @@ XE_DEV void keyed_union_item(const XeKeyed& K, uint32_t i) {
   uint32_t r = XE_NONE;
 #pragma unroll 1
   for (uint32_t j = 0; j < n; j++) {
-    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
+    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~XE_KLOG_FLAGS);
     if (d >= 0) { const uint32_t q = keyed_root(K, uint32_t(d)); r = q < r ? q : r; }
   }
   if (r == XE_NONE) return;
 #pragma unroll 1
   for (uint32_t j = 0; j < n; j++) {
-    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
+    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~XE_KLOG_FLAGS);
     if (d < 0) continue;
     const uint32_t q = keyed_root(K, uint32_t(d));
     if (q != r && xe_atomic_min32(K.dcomp + q, r) > r) xe_atomic_or32(K.changed, 1u);
@@ -2760,31 +2835,31 @@ XE_DEV void keyed_compress_item(const XeKeyed& K, uint32_t x) {
 XE_DEV void keyed_assign_item(const XeKeyed& K, uint32_t i, uint8_t* skip) {
   const uint32_t n = K.kcnt[i] < XE_KLOG ? K.kcnt[i] : XE_KLOG;
   uint32_t c = K.dcap;
-#pragma unroll 1
-  for (uint32_t j = 0; j < n && c == K.dcap; j++) {
-    const int64_t d = dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~1ull);
-    if (d >= 0) c = K.dcomp[d];
-  }
+  int64_t d[XE_KLOG];
+#pragma unroll
+  for (uint32_t j = 0; j < XE_KLOG; j++) d[j] = j < n ? dset_find(K, K.klog[uint64_t(i) * XE_KLOG + j] & ~XE_KLOG_FLAGS) : -1;
+#pragma unroll
+  for (uint32_t j = 0; j < XE_KLOG; j++)
+    if (c == K.dcap && d[j] >= 0) c = K.dcomp[d[j]];
   K.ckey[i] = c;
   skip[i] = c != K.dcap ? 1 : 0;
-  if (c != K.dcap) xe_atomic_add32(K.counts, 1u);
 }
-XE_DEV void keyed_starts_item(const XeKeyed& K, uint32_t p) {
-  if (p >= K.counts[0]) return;
-  if (p == 0 || K.okey[p] != K.okey[p - 1]) K.cbeg[xe_atomic_add32(K.counts + 1, 1u)] = p;
+// after the sort: nO = the number of packets on chains (sorted keys before the first "none")
+XE_DEV void keyed_nchain_item(const XeKeyed& K, uint32_t p) {
+  const bool on = K.okey[p] != K.dcap;
+  const bool next = p + 1 < K.n && K.okey[p + 1] != K.dcap;
+  if (on && !next) K.counts[0] = p + 1;
 }
-XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t e) {
-  const uint64_t* en = K.ins + uint64_t(e) * XE_INS_WORDS;
+// D slot x: a new HASH key held back by SPEC gets its slot record reserved
+XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x) {
+  if (!((XE_GP(const unsigned long long))K.dkid)[x]) return;
+  const uint64_t* en = K.dkey + uint64_t(x) * K.kw;
+  if (!(en[0] & XE_KEY_VALID) || (en[0] & 0x100ull)) return;  // not an insert / the nil key's own slot
   const uint32_t m = uint32_t(en[0] & 0xffu);
-  if (en[0] & 0x100ull) return;  // the nil key has its own slot
-  const XeDevMap M = maps[m];
   uint64_t kw[XE_MAX_KEY / 8];
 #pragma unroll
-  for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = en[1 + w];
-  const int64_t d = dset_find(K, xe_kid(m, xe_hash_words(kw, M.kwords, M.key_size)));
-  if (d < 0) { xe_atomic_or32(K.err, 4u); return; }
-  if (xe_atomic_cas32(K.drep + d, XE_NONE, e) != XE_NONE) return;  // another entry of this key reserves it
-  if (!hash_reserve(M, kw)) xe_atomic_or32(K.err, 2u);
+  for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w + 1 < K.kw ? en[1 + w] : 0;
+  if (!hash_reserve(maps[m], kw)) xe_atomic_or32(K.err, 2u);
 }
 XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t i) {
   switch (step) {
@@ -2792,37 +2867,47 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_UNION: keyed_union_item(K, i); break;
     case XE_KS_COMPRESS: keyed_compress_item(K, i); break;
     case XE_KS_ASSIGN: keyed_assign_item(K, i, skip); break;
-    case XE_KS_IOTA: K.cbeg[i] = i; break;
-    case XE_KS_STARTS: keyed_starts_item(K, i); break;
+    case XE_KS_IOTA: K.iota[i] = i; break;
+    case XE_KS_NCHAIN: keyed_nchain_item(K, i); break;
     case XE_KS_RESERVE: keyed_reserve_item(K, maps, i); break;
     default: break;
   }
 }
 
-// Chain-mode driver (XE_MODE_CHAIN, keyed ordered execution): thread g of the grid runs chains g,
-// g + nthreads, ... one after another, each chain's packets in packet order (order[cbeg[c]..] while
-// the sorted chain key stays the same). All lanes of a wave call body together until every lane of
-// the wave has run out of chains.
+// Chain-mode driver (XE_MODE_CHAIN, keyed ordered execution): thread g of the grid looks at sorted
+// positions g, g + nthreads, ... and runs the chain starting at each position where the sorted chain
+// key changes, its packets in packet order (order[p..] while the key stays the same). All lanes of a
+// wave call body together until every lane of the wave has run out of positions.
 template <class Body>
 XE_DEV void chain_packets(XeLane& L, const XeParams& P, uint32_t g, uint32_t nthreads, Body body) {
-  uint32_t c = g, p = 0, key = 0;
-  bool have = c < P.K.nchains;
-  if (have) { p = P.K.cbeg[c]; key = P.K.okey[p]; }
+  uint32_t q = g, p = 0, key = 0;  // q: the lane's next candidate start position (grid-stride)
+  bool have = false;
+  auto next_chain = [&]() {
+    have = false;
+#pragma unroll 1
+    while (q < P.K.nO) {
+      const uint32_t c = q;
+      q += nthreads;
+      if (c == 0 || P.K.okey[c] != P.K.okey[c - 1]) {
+        p = c;
+        key = P.K.okey[c];
+        have = true;
+        break;
+      }
+    }
+  };
+  next_chain();
 #pragma unroll 1
   for (;;) {
     if (!xe_ballot(have)) break;
     const uint32_t i = have ? P.K.order[p] : 0u;
     L.kchain = key;
     lane_reset(L, P, i, have);
-    key_begin(L);
+    key_begin(L, i);
     body(i, have);
     if (have) {
       p++;
-      if (p >= P.K.nO || P.K.okey[p] != key) {
-        c += nthreads;
-        have = c < P.K.nchains;
-        if (have) { p = P.K.cbeg[c]; key = P.K.okey[p]; }
-      }
+      if (p >= P.K.nO || P.K.okey[p] != key) next_chain();
     }
   }
 }
@@ -2854,7 +2939,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
       for (uint32_t j = 0; j < XE_KLOG; j++)
         if (j < L.kn) P.K.klog[uint64_t(i) * XE_KLOG + j] = L.klog[j];
     }
-    if (xe_ballot(valid && L.kwr) && xe_lane() == 0) xe_atomic_or32(P.flags, XE_FLAG_KEYED);
+    L.kany = L.kany || xe_ballot(valid && L.kwr) != 0;  // flagged once per wave (flush_wave_state)
   }
 #endif
   if (valid) {
@@ -2951,6 +3036,9 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   L.acc_steps = 0;
 #pragma unroll
   for (int st = 0; st < 8; st++) L.acc_status[st] = 0;
+#if XE_KEYED
+  L.kany = false;
+#endif
 }
 
 #if XE_GEN
@@ -3019,6 +3107,9 @@ XE_DEV void flush_wave_state(XeLane& L, const XeParams& P) {
   for (int o = 32; o > 0; o >>= 1) aw |= __shfl_xor(aw, o);
 #endif
   if (xe_lane() == 0 && aw) xe_atomic_or64(&L.rep[XE_REC_WIDTH0], aw);
+#if XE_KEYED
+  if (xe_lane() == 0 && L.kany) xe_atomic_or32(P.flags, XE_FLAG_KEYED);
+#endif
 #if defined(__HIPCC__)
   for (int o = 32; o > 0; o >>= 1) steps += __shfl_xor(steps, o);
 #endif

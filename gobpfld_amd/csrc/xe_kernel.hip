@@ -191,14 +191,30 @@ extern "C" __global__ void xe_keyed_kernel(XeKeyed K, const XeDevMap* maps, uint
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < items; i += uint64_t(gridDim.x) * blockDim.x)
     keyed_step(K, maps, skip, step, uint32_t(i));
 }
+// D keys per map (XE_KS_COUNT): a block histogram in LDS, one atomic per map per block
+extern "C" __global__ void xe_keyed_count_kernel(XeKeyed K) {
+  __shared__ unsigned int hist[64];
+  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t x = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; x < K.dcap; x += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t kid = K.dkid[x];
+    if (kid) atomicAdd(&hist[kid >> 58], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64 && hist[threadIdx.x]) atomicAdd(K.dcount + threadIdx.x, hist[threadIdx.x]);
+}
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s) {
   if (!items) return 0;
+  if (step == XE_KS_COUNT) {
+    hipLaunchKernelGGL(xe_keyed_count_kernel, dim3(1024), dim3(256), 0, s, *K);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   const uint32_t blocks = items / 256 + 1 < 8192 ? items / 256 + 1 : 8192;
   hipLaunchKernelGGL(xe_keyed_kernel, dim3(blocks), dim3(256), 0, s, *K, maps, skip, step, items);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-// (ckey, cbeg = 0..n-1) -> (okey, order), by chain key bits [0, end_bit); LSD radix sort is stable, so a
+// (ckey, iota = 0..n-1) -> (okey, order), by chain key bits [0, end_bit); LSD radix sort is stable, so a
 // chain's packets stay in packet order. scratch == nullptr: *bytes receives the scratch size.
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s) {
   size_t tmp = 0;
@@ -210,7 +226,7 @@ extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_b
     return 0;
   }
   if (*bytes < tmp) return -1;
-  return hipcub::DeviceRadixSort::SortPairs(scratch, tmp, K->ckey, K->okey, K->cbeg, K->order, int(n), 0, int(end_bit), s) ==
+  return hipcub::DeviceRadixSort::SortPairs(scratch, tmp, K->ckey, K->okey, K->iota, K->order, int(n), 0, int(end_bit), s) ==
                  hipSuccess
              ? 0
              : -1;

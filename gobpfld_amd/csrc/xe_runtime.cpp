@@ -173,13 +173,18 @@ int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* s
   return 0;
 }
 int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items, xe_stream_t) {
+  if (step == XE_KS_COUNT) {  // xe_kernel.hip xe_keyed_count_kernel
+    for (uint32_t x = 0; x < K->dcap; x++)
+      if (K->dkid[x]) K->dcount[K->dkid[x] >> 58]++;
+    return 0;
+  }
   for (uint32_t i = 0; i < items; i++) keyed_step(*K, maps, skip, step, i);  // xe_kernel.hip xe_keyed_kernel
   return 0;
 }
 int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
   if (!scratch) { *bytes = 8; return 0; }
   std::vector<std::pair<uint32_t, uint32_t>> v(n);
-  for (uint32_t i = 0; i < n; i++) v[i] = {K->ckey[i], K->cbeg[i]};
+  for (uint32_t i = 0; i < n; i++) v[i] = {K->ckey[i], K->iota[i]};
   std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
   return 0;
@@ -675,9 +680,10 @@ struct xe_vm {
   // last batch needed it, so the next one starts with the SPEC pass instead of a plain parallel run
   XeKeyed kd{};
   uint8_t* d_skip = nullptr;
-  uint32_t* d_ksmall = nullptr;  // [0..63] dcount, [64] err, [65] changed, [66..67] counts, [68] nins
+  uint32_t* d_ksmall = nullptr;  // XE_KS_WORDS counters (xe_internal.h layout)
   uint64_t keyed_n = 0;          // packets the per-packet arrays hold
-  uint32_t keyed_dcap = 0, keyed_ins = 0;
+  uint32_t keyed_dcap = 0, keyed_kw = 0;
+  uint32_t keyed_dnext = 0;      // D table size for the next keyed batch (from the last one's D size)
   void* d_ksort = nullptr;
   size_t d_ksort_cap = 0;
   bool keyed_hint = false;
@@ -686,42 +692,61 @@ struct xe_vm {
 // ---- keyed ordered execution buffers (XeKeyed), sized for n packets
 static void keyed_free(xe_vm* vm) {
   XeKeyed& K = vm->kd;
-  dev_free(K.klog); dev_free(K.kcnt); dev_free(K.ins); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.drep);
-  dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.cbeg);
+  dev_free(K.klog); dev_free(K.kcnt); dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.ikey);
+  dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.iota);
   dev_free(vm->d_skip); dev_free(vm->d_ksmall); dev_free(vm->d_ksort);
   K = XeKeyed{};
   vm->d_skip = nullptr; vm->d_ksmall = nullptr; vm->d_ksort = nullptr;
   vm->d_ksort_cap = 0;
   vm->keyed_n = 0;
-  vm->keyed_dcap = vm->keyed_ins = 0;
+  vm->keyed_dcap = vm->keyed_kw = 0;
 }
-static int keyed_alloc(xe_vm* vm, uint32_t n) {
-  if (vm->keyed_n >= n && vm->d_ksmall) return 0;
-  keyed_free(vm);
+// Per-packet arrays for n packets; the D table with dcap slots (its own size: it is probed at random by
+// every keyed access, so it is kept near the live D size — cache-resident — rather than 2n).
+static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
+  uint32_t kw = 1;  // dkey entry: map word + the longest HASH key
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].dkind == XE_DM_HASH) kw = std::max(kw, 1 + vm->maps[i].kwords);
   XeKeyed& K = vm->kd;
-  const uint64_t np = std::max<uint64_t>(n, 64);
-  uint32_t dcap = 4096;
-  while (dcap < 2 * np && dcap < (1u << 30)) dcap <<= 1;
-  const uint32_t ins = uint32_t(std::min<uint64_t>(np, 4u << 20));
-  bool bad = dev_alloc((void**)&K.klog, np * XE_KLOG * 8) || dev_alloc((void**)&K.kcnt, np * 4) ||
-             dev_alloc((void**)&K.ins, uint64_t(ins) * XE_INS_WORDS * 8) || dev_alloc((void**)&K.dkid, uint64_t(dcap) * 8) ||
-             dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4) || dev_alloc((void**)&K.drep, uint64_t(dcap) * 4) ||
-             dev_alloc((void**)&K.ckey, np * 4) || dev_alloc((void**)&K.okey, np * 4) || dev_alloc((void**)&K.order, np * 4) ||
-             dev_alloc((void**)&K.cbeg, np * 4) || dev_alloc((void**)&vm->d_skip, np) || dev_alloc((void**)&vm->d_ksmall, 128 * 4);
-  if (bad) { keyed_free(vm); return -1; }
-  K.ins_cap = ins;
+  if (vm->keyed_n < n || !vm->d_ksmall || vm->keyed_kw < kw) {
+    dev_free(K.klog); dev_free(K.kcnt); dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.iota);
+    dev_free(K.ikey); dev_free(vm->d_skip); dev_free(vm->d_ksmall);
+    K.klog = K.ikey = nullptr; K.kcnt = K.ckey = K.okey = K.order = K.iota = nullptr;
+    vm->d_skip = nullptr; vm->d_ksmall = nullptr;
+    vm->keyed_n = 0;
+    vm->keyed_dcap = 0;  // the D block is sized with the same key width
+    const uint64_t np = std::max<uint64_t>(n, 64);
+    if (dev_alloc((void**)&K.klog, np * XE_KLOG * 8) || dev_alloc((void**)&K.kcnt, np * 4) ||
+        dev_alloc((void**)&K.ikey, np * XE_KINS * kw * 8) ||
+        dev_alloc((void**)&K.ckey, np * 4) || dev_alloc((void**)&K.okey, np * 4) || dev_alloc((void**)&K.order, np * 4) ||
+        dev_alloc((void**)&K.iota, np * 4) || dev_alloc((void**)&vm->d_skip, np) ||
+        dev_alloc((void**)&vm->d_ksmall, XE_KS_WORDS * 4)) {
+      keyed_free(vm);
+      return -1;
+    }
+    vm->keyed_n = np;
+    K.dcount = vm->d_ksmall + XE_KS_DCOUNT;
+    K.err = vm->d_ksmall + XE_KS_ERR;
+    K.changed = vm->d_ksmall + XE_KS_CHANGED;
+    K.counts = vm->d_ksmall + XE_KS_NO;
+    K.cins = vm->d_ksmall + XE_KS_CINS;
+  }
+  if (vm->keyed_dcap != dcap || vm->keyed_kw < kw) {
+    dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp);
+    K.dkey = nullptr; K.dkid = nullptr; K.dcomp = nullptr;
+    vm->keyed_dcap = 0;
+    if (dev_alloc((void**)&K.dkey, uint64_t(dcap) * kw * 8) || dev_alloc((void**)&K.dkid, uint64_t(dcap) * 8) ||
+        dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4)) {
+      keyed_free(vm);
+      return -1;
+    }
+    vm->keyed_dcap = dcap;
+    vm->keyed_kw = kw;
+  }
+  K.kw = vm->keyed_kw;
   K.dcap = dcap;
-  K.dcount = vm->d_ksmall;
-  K.err = vm->d_ksmall + 64;
-  K.changed = vm->d_ksmall + 65;
-  K.counts = vm->d_ksmall + 66;
-  K.nins = vm->d_ksmall + 68;
-  vm->keyed_n = np;
-  vm->keyed_dcap = dcap;
-  vm->keyed_ins = ins;
   return 0;
 }
-
 
 namespace {
 
@@ -1874,9 +1899,16 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     }
 #endif
     auto klaunch = [&](const XeParams* p, uint32_t b) { return kjit ? launch_jit(kjit, p, b, 256, s) : launch_interp(p, b, 256, s); };
-    if (keyed_alloc(vm, n)) return fail(vm, XE_ERR_NOMEM, "device alloc (keyed execution)");
+    // D table: 4x the last keyed batch's D keys (first time: n / 4), at most 2n (D holds <= n keys)
+    uint32_t dmax = 4096, dcap = 4096;
+    while (dmax < 2ull * n && dmax < (1u << 30)) dmax <<= 1;
+    const uint64_t dwant = vm->keyed_dnext ? vm->keyed_dnext : std::max<uint64_t>(4096, n / 4);
+    while (dcap < dwant && dcap < dmax) dcap <<= 1;
+    if (keyed_alloc(vm, n, dcap)) return fail(vm, XE_ERR_NOMEM, "device alloc (keyed execution)");
     XeKeyed K = vm->kd;
-    if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, 128 * 4, s)) return fail(vm, XE_ERR_DEVICE, "keyed reset");
+    K.n = n;
+    if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, XE_KS_WORDS * 4, s))
+      return fail(vm, XE_ERR_DEVICE, "keyed reset");
     const uint32_t grid = parallel_grid(vm, kjit, general, n, P.nmaps);
     XeParams X = P;
     if (general && ensure_arena(vm, false, grid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
@@ -1892,52 +1924,80 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       used_out = XE_MODE_PARALLEL;
       return 0;
     }
-    // 2. build: D, chains (union-find rounds), each packet's chain, the sorted order, chain starts
+    // 2. build: D, chains (union-find rounds), each packet's chain, the sorted order
     auto step = [&](uint32_t st, uint32_t items) { return launch_keyed(&K, vm->d_maps, vm->d_skip, st, items, s); };
-    uint32_t small[128];
-    auto read_small = [&]() { return d2h(small, vm->d_ksmall, sizeof small, s) || dsync(s); };
+    std::vector<uint32_t> small(XE_KS_WORDS);
+    auto read_small = [&]() { return d2h(small.data(), vm->d_ksmall, XE_KS_WORDS * 4, s) || dsync(s); };
     if (step(XE_KS_DSET, n)) return fail(vm, XE_ERR_DEVICE, "keyed build");
     for (int round = 0;; round++) {
       if (round >= 64) return rollback(false) ? -1 : 1;
       if (dmemset(K.changed, 0, 4, s) || step(XE_KS_UNION, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
-      if (!small[65]) break;
+      if (!small[XE_KS_CHANGED]) break;
     }
-    if (step(XE_KS_COMPRESS, K.dcap) || step(XE_KS_ASSIGN, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
-    if (small[64] || small[68] > K.ins_cap) return rollback(false) ? -1 : 1;  // key log or insert log overflow
+    if (step(XE_KS_COMPRESS, K.dcap) || step(XE_KS_ASSIGN, n) || step(XE_KS_COUNT, K.dcap) || read_small())
+      return fail(vm, XE_ERR_DEVICE, "keyed build");
+    if (small[XE_KS_ERR] & 8u) {  // D outgrew its table: once more with room for every packet's key
+      vm->keyed_dnext = dmax;
+      if (dcap < dmax) return rollback(false) ? -1 : 2;
+    }
+    if (small[XE_KS_ERR]) return rollback(false) ? -1 : 1;  // key log overflow
+    {
+      uint64_t nd = 0;
+      for (uint32_t i = 0; i < 64; i++) nd += small[XE_KS_DCOUNT + i];
+      uint64_t next = 4096;
+      while (next < 4 * nd && next < dmax) next <<= 1;
+      vm->keyed_dnext = uint32_t(next);
+    }
     // a HASH insert can fail for capacity only in an order-dependent way: every key of D fits
-    for (size_t i = 1; i < vm->maps.size(); i++) {
+    for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];
-      if (m.dkind != XE_DM_HASH || i >= 64 || !small[i]) continue;
+      const uint64_t nd = small[XE_KS_DCOUNT + i];
+      if (m.dkind != XE_DM_HASH || !nd) continue;
       uint32_t cnt = 0;
       if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
-      if (uint64_t(cnt) + small[i] > m.def.max_entries) return rollback(false) ? -1 : 1;
+      if (uint64_t(cnt) + nd > m.def.max_entries) return rollback(false) ? -1 : 1;
     }
-    const uint32_t nO = small[66];
     uint32_t end_bit = 1;
     while ((1ull << end_bit) <= K.dcap) end_bit++;
     size_t sb = 0;
     if (step(XE_KS_IOTA, n) || launch_keyed_sort(&K, n, end_bit, nullptr, &sb, s) ||
         ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb) || launch_keyed_sort(&K, n, end_bit, vm->d_ksort, &sb, s))
       return fail(vm, XE_ERR_DEVICE, "keyed sort");
-    K.nO = nO;
-    if (step(XE_KS_STARTS, nO) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
-    K.nchains = small[67];
+    if (step(XE_KS_NCHAIN, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
+    K.nO = small[XE_KS_NO];
     // 3. back to the start state; reserve a slot record for every new HASH key of D
     if (rollback(false) || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
-    if (step(XE_KS_RESERVE, small[68]) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");
-    if (small[64]) return rollback(true) ? -1 : 1;
-    // 4. the packets on no chain, in parallel
+    if (step(XE_KS_RESERVE, K.dcap) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");
+    if (small[XE_KS_ERR]) return rollback(true) ? -1 : 1;
+    // 4. the packets on no chain, in parallel (the fast kernel: the skip mask is its only keyed input)
     X.mode = XE_MODE_PARALLEL;
     X.K = K;
     X.K.skip = vm->d_skip;
-    if (nO < n && (klaunch(&X, grid) || fold())) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed parallel)");
+    if (K.nO < n) {
+      XeParams Y = X;
+      const uint32_t pgrid = parallel_grid(vm, jit, general, n, P.nmaps);
+      if (general && ensure_arena(vm, false, pgrid * 256, Y.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+      if (launch(&Y, pgrid, 256) || fold()) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed parallel)");
+    }
     // 5. the chains, one lane each, in packet order
     X.mode = XE_MODE_CHAIN;
     X.K.skip = nullptr;
-    const uint32_t cgrid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (K.nchains + 255) / 256));
+    const uint32_t cgrid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (K.nO + 255) / 256));
+    if (general && ensure_arena(vm, false, cgrid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     if (klaunch(&X, cgrid)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
-    if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
+    if (read_aux() || read_small()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
     if (run_conflict(red, P.nmaps)) return rollback(true) ? -1 : 1;  // a packet left its chain / an order-dependent add
+    // the chains' inserts into the map counts
+    for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
+      HostMap& m = vm->maps[i];
+      uint32_t add = 0;
+      for (uint32_t k = 0; k < XE_KSTRIPES; k++) add += small[XE_KS_CINS + i * XE_KSTRIPES + k];
+      if (m.dkind != XE_DM_HASH || !add) continue;
+      uint32_t cnt = 0;
+      if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+      cnt += add;
+      if (h2d(m.d_count, &cnt, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+    }
     vm->last_grid = grid;
     used_out = XE_MODE_KEYED;
     return 0;
@@ -1954,7 +2014,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (int rc = sequential(kms)) return rc;
   } else if (keyed_ok && vm->keyed_hint) {
     // the last batch wrote map entries: straight to the keyed path
-    const int r = keyed(used);
+    int r = keyed(used);
+    if (r == 2) r = keyed(used);  // its D table was too small
     if (r < 0) return r;
     if (r == 1) {
       vm->keyed_refused = true;
@@ -1984,6 +2045,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY) && !vm->keyed_refused) {
         vm->t2.rec(s);
         r = keyed(used);
+        if (r == 2) r = keyed(used);  // its D table was too small
         if (r < 0) return r;
         vm->keyed_refused = r == 1;
         if (r == 0) {

@@ -114,6 +114,19 @@ def prog_first_seen():
     return a.assemble()
 
 
+def prog_many_keys():
+    """ARRAY(16384 x u64): element (bytes 0-1 & 0x3fff) := byte 2 (a plain store). Thousands of distinct
+    written keys: more than the first keyed batch's D table holds, so the path retries with room for
+    one key per packet."""
+    a = Asm()
+    a.ldx(4, 6, 1, 0).ldx(2, 8, 6, 0).alu64(AND, 8, 0x3FFF).ldx(1, 9, 6, 2)
+    a.stx(4, 10, -4, 8).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "out", imm=0)
+    a.stx(8, 0, 0, 9)
+    a.label("out").mov64(0, XDP_PASS).exit()
+    return a.assemble()
+
+
 def _last_len_maps():
     entries = {0: [(np.uint32(k).tobytes(), bytes(16)) for k in range(0, 32, 2)]}  # even keys preloaded
     return [(MapDef(MAP_HASH, 4, 16, 64), None)], entries
@@ -139,6 +152,12 @@ def test_keyed_hostsim(oracle_lib, hostsim_lib, case):
     prog, maps, entries = CASES[case]()
     umem, descs = packets(3000, 64, seed=21)
     _check(hostsim_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_KEYED, case)
+
+
+def test_keyed_d_table_retry_hostsim(oracle_lib, hostsim_lib):
+    umem, descs = packets(12000, 64, seed=25)
+    _check(hostsim_lib, oracle_lib, prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, umem, descs,
+           MODE_KEYED, "many_keys")
 
 
 def test_keyed_escape_hostsim(oracle_lib, hostsim_lib):
@@ -272,3 +291,10 @@ def test_keyed_batches_device(gpu_lib, oracle_lib):
 @pytest.mark.gpu
 def test_keyed_tombstones_device(gpu_lib, oracle_lib):
     _tombstones(gpu_lib, oracle_lib, 50000)
+
+
+@pytest.mark.gpu
+def test_keyed_d_table_retry_device(gpu_lib, oracle_lib):
+    umem, descs = packets(60000, 64, seed=26)
+    _check(gpu_lib, oracle_lib, prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, umem, descs,
+           MODE_KEYED, "many_keys")

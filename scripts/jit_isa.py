@@ -3,6 +3,7 @@
 compiles it with hipcc for gfx950 (-S), and prints resource usage + instruction-class counts.
 
   python scripts/jit_isa.py c2 [-DXE_PEND_MODE=2 ...]
+  python scripts/jit_isa.py c3learn --keyed     (the keyed variant: XE_MODE_SPEC / XE_MODE_CHAIN)
 """
 import ctypes as C
 import re
@@ -18,7 +19,8 @@ from gobpfld_amd import workloads as W  # noqa: E402
 from gobpfld_amd._native import PRODUCT_LIB  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c2"
-defs = sys.argv[2:]
+defs = [a for a in sys.argv[2:] if a != "--keyed"]
+keyed = "--keyed" in sys.argv[2:]
 lib = C.CDLL(str(PRODUCT_LIB))
 lib.xe_translate_uops.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
 lib.xe_jit_source.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
@@ -40,7 +42,9 @@ for mdef, _ in W.workload_maps(name):
 g = np.asarray(geom, dtype=np.uint32)
 lib.xe_jit_source_geom(u.ctypes.data, n, g.ctypes.data, len(geom) // 7, buf, len(buf))
 src = buf.value.decode()
-out = Path("/tmp") / f"xe_jit_{name}"
+if keyed:
+    src = src.replace("#define XE_KEYED 0", "#define XE_KEYED 1")
+out = Path("/tmp") / f"xe_jit_{name}{'_keyed' if keyed else ''}"
 out.mkdir(exist_ok=True)
 (out / "k.hip").write_text('#include <hip/hip_runtime.h>\n' + src)
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-std=c++17",

@@ -216,7 +216,7 @@ XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
 #define XE_KINS 2u            // ikey slots per packet (more held-back inserts: the one-lane replay)
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
 enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
-                  XE_KS_COUNT };
+                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG };
 // Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
 // a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
 // a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
@@ -226,6 +226,7 @@ enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_
 #define XE_KS_ERR 64                        // build errors
 #define XE_KS_CHANGED 65                    // union-find round changed something
 #define XE_KS_NO 66                         // packets on chains
+#define XE_KS_LONG 67                       // some chain holds more than half the batch
 #define XE_KS_CINS 128                      // [64 maps][XE_KSTRIPES] inserts the chains made
 #define XE_KS_WORDS (128 + 64 * XE_KSTRIPES)
 #define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid
@@ -239,6 +240,7 @@ struct XeKeyed {
   uint32_t kw;         // words of a dkey entry: 1 + the longest HASH key's words
   uint64_t* dkid;      // D table: key ids (0 = free)
   uint32_t* dcomp;     // D table: chain (union-find parent, then the root)
+  uint32_t* cstart;    // [dcap] position of chain (root) c's first packet in order[]
   uint64_t* dkey;      // D table: [dcap * kw] a held-back insert's key (word 0: map | 0x100 nil | VALID)
   uint64_t* ikey;      // [n * XE_KINS * kw] the key words of a packet's held-back inserts (SPEC)
   uint32_t* dcount;    // [64] D keys per map (HASH capacity bound)

@@ -2861,6 +2861,14 @@ XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t 
   for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w + 1 < K.kw ? en[1 + w] : 0;
   if (!hash_reserve(maps[m], kw)) xe_atomic_or32(K.err, 2u);
 }
+// chain lengths: a chain holding more than half the batch runs faster as the staged one-lane replay
+XE_DEV void keyed_cstart_item(const XeKeyed& K, uint32_t p) {
+  if (p == 0 || K.okey[p] != K.okey[p - 1]) K.cstart[K.okey[p]] = p;
+}
+XE_DEV void keyed_clong_item(const XeKeyed& K, uint32_t p) {
+  if (p + 1 < K.nO && K.okey[p + 1] == K.okey[p]) return;  // not a chain's last packet
+  if (uint64_t(p + 1 - K.cstart[K.okey[p]]) * 2 > K.n) K.counts[1] = 1;
+}
 XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t i) {
   switch (step) {
     case XE_KS_DSET: keyed_dset_item(K, i); break;
@@ -2870,6 +2878,8 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_IOTA: K.iota[i] = i; break;
     case XE_KS_NCHAIN: keyed_nchain_item(K, i); break;
     case XE_KS_RESERVE: keyed_reserve_item(K, maps, i); break;
+    case XE_KS_CSTART: keyed_cstart_item(K, i); break;
+    case XE_KS_CLONG: keyed_clong_item(K, i); break;
     default: break;
   }
 }

@@ -693,6 +693,7 @@ struct xe_vm {
 static void keyed_free(xe_vm* vm) {
   XeKeyed& K = vm->kd;
   dev_free(K.klog); dev_free(K.kcnt); dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.ikey);
+  dev_free(K.cstart);
   dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.iota);
   dev_free(vm->d_skip); dev_free(vm->d_ksmall); dev_free(vm->d_ksort);
   K = XeKeyed{};
@@ -732,11 +733,11 @@ static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
     K.cins = vm->d_ksmall + XE_KS_CINS;
   }
   if (vm->keyed_dcap != dcap || vm->keyed_kw < kw) {
-    dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp);
-    K.dkey = nullptr; K.dkid = nullptr; K.dcomp = nullptr;
+    dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.cstart);
+    K.dkey = nullptr; K.dkid = nullptr; K.dcomp = K.cstart = nullptr;
     vm->keyed_dcap = 0;
     if (dev_alloc((void**)&K.dkey, uint64_t(dcap) * kw * 8) || dev_alloc((void**)&K.dkid, uint64_t(dcap) * 8) ||
-        dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4)) {
+        dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4) || dev_alloc((void**)&K.cstart, uint64_t(dcap) * 4)) {
       keyed_free(vm);
       return -1;
     }
@@ -1965,6 +1966,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       return fail(vm, XE_ERR_DEVICE, "keyed sort");
     if (step(XE_KS_NCHAIN, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
     K.nO = small[XE_KS_NO];
+    // one chain with more than half the packets (a hot key written by most of them): its lane would
+    // take longer than the staged one-lane replay of the whole batch
+    if (step(XE_KS_CSTART, K.nO) || step(XE_KS_CLONG, K.nO) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
+    if (small[XE_KS_LONG]) return rollback(false) ? -1 : 1;
     // 3. back to the start state; reserve a slot record for every new HASH key of D
     if (rollback(false) || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
     if (step(XE_KS_RESERVE, K.dcap) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");

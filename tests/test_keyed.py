@@ -56,11 +56,12 @@ def prog_rate_limit():
 
 
 def prog_two_keys():
-    """HASH(4 B -> u64) learning counters for two keys per packet: (byte 0 & 15) and 16 + (byte 1 & 15).
-    A miss inserts 1, a hit adds 1. Packets join the chains of both keys (union-find)."""
+    """HASH(4 B -> u64) learning counters for two keys per packet: (byte 0 & 15) and 16 + (byte 0 & 15).
+    A miss inserts 1, a hit adds 1. Each packet joins the chains of both its keys (union-find): 16
+    chains of two keys each."""
     a = Asm()
     a.ldx(4, 6, 1, 0)
-    for k, (byte, base) in enumerate(((0, 0), (1, 16))):
+    for k, (byte, base) in enumerate(((0, 0), (0, 16))):
         a.ldx(1, 8, 6, byte).alu64(AND, 8, 15).add64(8, base)
         a.stx(4, 10, -4, 8).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
         a.jmp(JEQ, 0, f"ins{k}", imm=0)
@@ -96,12 +97,12 @@ def prog_escape():
 
 
 def prog_first_seen():
-    """HASH(4 B -> u64): key A = byte 0 & 7; on a miss insert A and a second key B = 100 + (byte 1 & 63).
-    The SPEC pass sees every A absent, so it reserves a B for every packet; in packet order only the
-    first packet of each A inserts its B. The unused reservations stay behind as tombstones."""
+    """HASH(4 B -> u64): key A = byte 0 & 7; on a miss insert A and a second key B = 100 + (byte 0 & 63)
+    (8 Bs per A: 8 chains). The SPEC pass sees every A absent, so it reserves every B; in packet order
+    only the first packet of each A inserts its B. The unused reservations stay behind as tombstones."""
     a = Asm()
     _key_byte(a, 8, 0, 7)
-    a.ldx(1, 9, 6, 1).alu64(AND, 9, 63).add64(9, 100)
+    a.ldx(1, 9, 6, 0).alu64(AND, 9, 63).add64(9, 100)
     a.stx(4, 10, -4, 8).ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
     a.jmp(JEQ, 0, "ins", imm=0)
     a.mov64(1, 1).xadd(8, 0, 0, 1).ja("out")
@@ -158,6 +159,14 @@ def test_keyed_d_table_retry_hostsim(oracle_lib, hostsim_lib):
     umem, descs = packets(12000, 64, seed=25)
     _check(hostsim_lib, oracle_lib, prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, umem, descs,
            MODE_KEYED, "many_keys")
+
+
+def test_keyed_hot_key_replays_hostsim(oracle_lib, hostsim_lib):
+    """Every packet reads and writes one ARRAY element: one chain of the whole batch, which goes to the
+    staged one-lane replay instead (exact either way)."""
+    umem, descs = packets(3000, 64, seed=27, fill=3)  # byte 0 & 7 = 3 for every packet
+    _check(hostsim_lib, oracle_lib, prog_rate_limit(), [(MapDef(MAP_ARRAY, 4, 8, 8), None)], None, umem, descs,
+           MODE_SEQUENTIAL, "hot key")
 
 
 def test_keyed_escape_hostsim(oracle_lib, hostsim_lib):

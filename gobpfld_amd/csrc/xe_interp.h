@@ -2995,8 +2995,13 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   }
   // batch statistics: per-lane step sums and wave-uniform status counts, flushed once per wave
   L.acc_steps += valid ? steps : 0;
+  // status histogram: one ballot when every packet of the chunk ended OK (the common case)
+  const unsigned long long vb = xe_ballot(valid), bad = xe_ballot(valid && status != XE_ST_OK);
+  L.acc_status[0] += uint32_t(__builtin_popcountll(vb & ~bad));
+  if (bad) {
 #pragma unroll
-  for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
+    for (int st = 1; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
+  }
 }
 
 // the stores lane_finish deferred (all lanes of the wave together)

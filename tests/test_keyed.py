@@ -128,6 +128,29 @@ def prog_many_keys():
     return a.assemble()
 
 
+def prog_learn_in_call():
+    """prog_two_keys' learning step for key (byte 0 & 15) inside a bpf-to-bpf call (the general lane
+    model, emulator/inst_call_bpf.go:18-44), and the packet's byte 3 := 0x5a (a packet write)."""
+    a = Asm()
+    a.ldx(4, 6, 1, 0)
+    a.mov64(2, 0x5A).stx(1, 6, 3, 2)
+    a.ldx(1, 8, 6, 0).alu64(AND, 8, 15)
+    a.stx(4, 10, -4, 8)
+    a.mov64(1, src=10).add64(1, -4)
+    a.call_bpf("learn")
+    a.mov64(0, XDP_PASS).exit()
+    a.label("learn")                        # r1 = key pointer (caller's frame)
+    a.mov64(6, src=1)
+    a.ld_map(1, 1).mov64(2, src=6).call(1)
+    a.jmp(JEQ, 0, "ins", imm=0)
+    a.mov64(1, 1).xadd(8, 0, 0, 1).mov64(0, 0).exit()
+    a.label("ins")
+    a.st(8, 10, -8, 1)
+    a.ld_map(1, 1).mov64(2, src=6).mov64(3, src=10).add64(3, -8).mov64(4, 0).call(2)
+    a.mov64(0, 0).exit()
+    return a.assemble()
+
+
 def _last_len_maps():
     entries = {0: [(np.uint32(k).tobytes(), bytes(16)) for k in range(0, 32, 2)]}  # even keys preloaded
     return [(MapDef(MAP_HASH, 4, 16, 64), None)], entries
@@ -167,6 +190,23 @@ def test_keyed_hot_key_replays_hostsim(oracle_lib, hostsim_lib):
     umem, descs = packets(3000, 64, seed=27, fill=3)  # byte 0 & 7 = 3 for every packet
     _check(hostsim_lib, oracle_lib, prog_rate_limit(), [(MapDef(MAP_ARRAY, 4, 8, 8), None)], None, umem, descs,
            MODE_SEQUENTIAL, "hot key")
+
+
+def test_keyed_call_and_packet_write_hostsim(oracle_lib, hostsim_lib):
+    umem, descs = packets(2500, 64, seed=28)
+    _check(hostsim_lib, oracle_lib, prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, umem, descs,
+           MODE_KEYED, "call + packet write")
+
+
+@pytest.mark.parametrize("case", ["last_len", "two_keys"])
+def test_keyed_register_records_hostsim(oracle_lib, hostsim_lib, case):
+    """With R0-R9 records requested (no read-modify-write lifting), every chain packet's record too."""
+    prog, maps, entries = CASES[case]()
+    umem, descs = packets(2000, 64, seed=29)
+    a = run_one(hostsim_lib, prog, maps, umem, descs, entries=entries, regs=True)
+    b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=True)
+    assert_same(a, b, case)
+    assert a[0].stats["mode_used"] == MODE_KEYED
 
 
 def test_keyed_escape_hostsim(oracle_lib, hostsim_lib):
@@ -307,3 +347,23 @@ def test_keyed_d_table_retry_device(gpu_lib, oracle_lib):
     umem, descs = packets(60000, 64, seed=26)
     _check(gpu_lib, oracle_lib, prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, umem, descs,
            MODE_KEYED, "many_keys")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", [1, 0], ids=["interp", "auto"])
+def test_keyed_call_and_packet_write_device(gpu_lib, oracle_lib, engine):
+    umem, descs = packets(50000, 64, seed=30)
+    _check(gpu_lib, oracle_lib, prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, umem, descs,
+           MODE_KEYED, "call + packet write", Settings(engine=engine))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", [1, 2], ids=["interp", "jit"])
+@pytest.mark.parametrize("case", ["last_len", "two_keys"])
+def test_keyed_register_records_device(gpu_lib, oracle_lib, case, engine):
+    prog, maps, entries = CASES[case]()
+    umem, descs = packets(40000, 64, seed=31)
+    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, regs=True, settings=Settings(engine=engine))
+    b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=True)
+    assert_same(a, b, case)
+    assert a[0].stats["mode_used"] == MODE_KEYED

@@ -211,6 +211,14 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #define XE_KEYED 1
 #endif
 
+// status histogram with one ballot for an all-OK chunk; the skip mask in parallel passes (A/B knobs)
+#ifndef XE_HIST_FAST
+#define XE_HIST_FAST 1
+#endif
+#ifndef XE_SKIP_MASK
+#define XE_SKIP_MASK 1
+#endif
+
 // maps whose read / atomic footprints a lane keeps in registers (the rest OR straight into the wave's
 // record); a per-program kernel sets it to the VM's map count
 #ifndef XE_FP_MAPS
@@ -2688,7 +2696,9 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
 // body(i, valid) runs the staged packet and calls lane_finish; all lanes call it together.
 // packet i runs in this parallel pass (the keyed path's pass leaves out the packets on chains)
 XE_DEV bool pkt_in_pass(const XeParams& P, uint32_t i) {
+#if XE_SKIP_MASK
   if (P.K.skip && i < P.n && ((XE_GP(const uint8_t))P.K.skip)[i]) return false;
+#endif
   return i < P.n;
 }
 // the key log of the lane's next packet starts empty
@@ -2995,6 +3005,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
   }
   // batch statistics: per-lane step sums and wave-uniform status counts, flushed once per wave
   L.acc_steps += valid ? steps : 0;
+#if XE_HIST_FAST
   // status histogram: one ballot when every packet of the chunk ended OK (the common case)
   const unsigned long long vb = xe_ballot(valid), bad = xe_ballot(valid && status != XE_ST_OK);
   L.acc_status[0] += uint32_t(__builtin_popcountll(vb & ~bad));
@@ -3002,6 +3013,10 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 #pragma unroll
     for (int st = 1; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
   }
+#else
+#pragma unroll
+  for (int st = 0; st < 8; st++) L.acc_status[st] += uint32_t(__builtin_popcountll(xe_ballot(valid && status == st)));
+#endif
 }
 
 // the stores lane_finish deferred (all lanes of the wave together)

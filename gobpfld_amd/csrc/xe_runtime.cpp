@@ -466,6 +466,16 @@ uint32_t next_pow2(uint64_t v) {
   return p;
 }
 
+// Slot count of a device hash table: a power of two >= 2 x MaxEntries (at most half full), or, when
+// that no longer fits the 23-bit slot field of a value handle (xe_h_make), the largest table that does
+// (2^22 slots; probes run longer above half load, every entry still has a slot: MaxEntries <= cap).
+uint32_t hash_cap(uint32_t max_entries) {
+  uint32_t cap = next_pow2(uint64_t(max_entries) * 2);
+  const uint32_t lim = 1u << (XE_H_SLOT_BITS - 1);
+  if (cap > lim && max_entries <= lim) cap = lim;
+  return cap;
+}
+
 constexpr uint32_t kAsyncDepth = 3;  // pipelined batches in flight per VM (xe_run_batch_device_async)
 
 struct HostMap {
@@ -1256,8 +1266,8 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
     case XE_MAP_HASH: case XE_MAP_PERCPU_HASH: case XE_MAP_HASH_OF_MAPS:
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_HASH;
-      m.cap = next_pow2(uint64_t(def->max_entries) * 2);
-      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 2M)");
+      m.cap = hash_cap(def->max_entries);
+      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 4M)");
       m.kwords = (def->key_size + 7) / 8;
       m.vals_bytes = uint64_t(m.cap + 1) * def->value_size;
       m.keys.assign(size_t(m.cap + 1) * m.kwords, 0);
@@ -1266,8 +1276,8 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
     case XE_MAP_LRU_HASH: case XE_MAP_LRU_PERCPU_HASH:
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_LRU;
-      m.cap = next_pow2(uint64_t(def->max_entries) * 2);
-      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 2M)");
+      m.cap = hash_cap(def->max_entries);
+      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 4M)");
       m.kwords = (def->key_size + 7) / 8;
       break;
     case XE_MAP_QUEUE: case XE_MAP_STACK:

@@ -120,7 +120,8 @@ extern "C" {
 #define XE_ENGINE_JIT 2    /* per-program kernel only (error if it cannot be built) */
 
 /* run modes */
-#define XE_MODE_AUTO 0       /* parallel, verified; falls back to ordered device execution on conflict */
+#define XE_MODE_AUTO 0       /* parallel, verified; on conflict: map-entry writes as per-key chains  */
+                             /* (XE_MODE_KEYED), anything else ordered device execution            */
 #define XE_MODE_PARALLEL 1   /* parallel only; conflicts reported in stats, results kept            */
 #define XE_MODE_SEQUENTIAL 2 /* exact packet order on one device lane                             */
 #define XE_MODE_KEYED 3      /* (xe_batch_stats.mode_used only) map-entry writes: per-key chains  */
@@ -293,7 +294,8 @@ int xe_map_delta_lane(xe_vm* vm, int32_t map_idx, uint32_t* lane_bytes);
  * map m = 1..nmaps three words: read mask, atomic-add mask (64 field positions of a value) and the
  * width classes of its adds (bit 0: 1 B, 1: 2 B, 2: 4 B, 3: 8 B). nwords = 1 + 3 * nmaps. */
 #define XE_FPF_ORDERED 1    /* a lane needed a non-commutative map write */
-#define XE_FPF_SEQUENTIAL 2 /* the results come from the exact ordered replay (map writes in order) */
+#define XE_FPF_SEQUENTIAL 2 /* the results come from the exact ordered replay or the keyed chains   */
+                            /* (map writes in order)                                               */
 #define XE_FPF_UNALIGNED 4  /* a map add was not aligned to its own width */
 #define XE_FPF_EPOCH 8      /* the record covers a shard epoch (xe_epoch_begin): several batches */
 int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords);

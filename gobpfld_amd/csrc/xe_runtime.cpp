@@ -476,7 +476,8 @@ uint32_t hash_cap(uint32_t max_entries) {
   return cap;
 }
 
-constexpr uint32_t kAsyncDepth = 3;  // pipelined batches in flight per VM (xe_run_batch_device_async)
+constexpr uint32_t kAsyncDepth = 3;
+constexpr uint32_t kKeyedBackoff = 8;  // order-dependent batches that skip the keyed path after a refusal  // pipelined batches in flight per VM (xe_run_batch_device_async)
 
 struct HostMap {
   xe_map_def def{};
@@ -697,7 +698,9 @@ struct xe_vm {
   void* d_ksort = nullptr;
   size_t d_ksort_cap = 0;
   bool keyed_hint = false;
-  bool keyed_refused = false;  // the keyed path refused the last order-dependent batch: go straight to the replay
+  // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
+  // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
+  uint32_t keyed_backoff = 0;
 };
 // ---- keyed ordered execution buffers (XeKeyed), sized for n packets
 static void keyed_free(xe_vm* vm) {
@@ -2033,7 +2036,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (r == 2) r = keyed(used);  // its D table was too small
     if (r < 0) return r;
     if (r == 1) {
-      vm->keyed_refused = true;
+      vm->keyed_backoff = kKeyedBackoff;
       used = XE_MODE_SEQUENTIAL;
       if (int rc = sequential(kms)) return rc;
     }
@@ -2057,12 +2060,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       // keyed path, everything else (and what the keyed path refuses) the replay in packet order
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
       int r = 1;
-      if (keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY) && !vm->keyed_refused) {
+      const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY);
+      if (try_keyed && vm->keyed_backoff) vm->keyed_backoff--;
+      else if (try_keyed) {
         vm->t2.rec(s);
         r = keyed(used);
         if (r == 2) r = keyed(used);  // its D table was too small
         if (r < 0) return r;
-        vm->keyed_refused = r == 1;
+        if (r == 1) vm->keyed_backoff = kKeyedBackoff;
         if (r == 0) {
           vm->t1.rec(s);
           if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "sync");
@@ -2074,7 +2079,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         if (int rc = sequential(kms)) return rc;
       }
     } else if (!conflict) {
-      vm->keyed_refused = false;
+      vm->keyed_backoff = 0;
     }
   }
   vm->keyed_hint = used == XE_MODE_KEYED;

@@ -84,6 +84,11 @@ _SIGS = {
     "run_batch_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
     "run_batch_device_async": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
     "sync": (C.c_int, [P]),
+    "prepare": (C.c_int, [P]),
+    "debug_set_schedule": (C.c_int, [P, C.c_uint32]),
+    "set_kernel_cache": (C.c_int, [C.c_char_p]),
+    "kernel_source": (C.c_int, [P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "compile_kernel_source": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
     "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
@@ -116,10 +121,11 @@ HEADER_SYMBOLS = [
     "xe_default_settings", "xe_create", "xe_destroy", "xe_last_error", "xe_add_raw_program",
     "xe_set_entrypoint", "xe_add_map", "xe_map_lookup", "xe_map_update", "xe_map_delete",
     "xe_map_count", "xe_map_dump", "xe_map_dump_list", "xe_map_lru_order", "xe_map_push", "xe_map_update_batch", "xe_run_batch_device", "xe_run_batch_host",
-    "xe_run_batch_device_async", "xe_sync", "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
+    "xe_run_batch_device_async", "xe_sync", "xe_prepare", "xe_map_values_bytes", "xe_map_delta", "xe_map_apply_delta", "xe_map_delta_lane", "xe_footprint", "xe_version",
     "xe_device_count", "xe_shard_check", "xe_epoch_begin", "xe_epoch_end", "xe_map_state_bytes", "xe_map_state_export",
     "xe_map_state_import",
-    "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error",
+    "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error", "xe_debug_set_schedule",
+    "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h
 

@@ -216,7 +216,7 @@ XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
 #define XE_KINS 2u            // ikey slots per packet (more held-back inserts: the one-lane replay)
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
 enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
-                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG };
+                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW };
 // Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
 // a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
 // a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
@@ -338,6 +338,10 @@ struct XeParams {
   uint32_t seq_prefetch;
   // keyed ordered execution (XE_MODE_SPEC / XE_MODE_CHAIN, and the skip mask of its parallel pass)
   XeKeyed K;
+  // chunk -> wave schedule of the parallel pass (xe_debug_set_schedule): 0 = wave w walks chunks
+  // w, w + nwaves, ...; s > 0 = the walk visits chunk (nchunks - 1 - c + s) mod nchunks instead (a
+  // permutation; the results may not depend on it)
+  uint32_t sched;
 };
 
 // Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in

@@ -2715,6 +2715,12 @@ XE_DEV void key_begin(XeLane& L, uint32_t i) {
 #endif
 }
 
+// first packet of the c-th chunk of the walk (P.sched: a permuted chunk order, for determinism tests)
+XE_DEV uint32_t chunk_base(const XeParams& P, uint32_t c, uint32_t nchunks) {
+  if (P.sched && c < nchunks) c = uint32_t((uint64_t(nchunks) - 1 - c + P.sched) % nchunks);
+  return c * XE_WAVE;
+}
+
 template <class Body>
 XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32_t nwaves, Body body) {
   const uint32_t lane = uint32_t(xe_lane());
@@ -2723,13 +2729,13 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   if (c >= nchunks) return;
   // an earlier pipelined batch is being replayed in order: this one re-runs afterwards
   if (P.poison && xe_readfirst(int(xe_load_relaxed32(const_cast<unsigned int*>(P.poison))))) return;
-  uint32_t i0 = c * XE_WAVE + lane;
+  uint32_t i0 = chunk_base(P, c, nchunks) + lane;
   bool v0 = pkt_in_pass(P, i0);
   uint64_t a0;
   uint32_t l0;
   desc_fetch(P, i0, v0, a0, l0);
   uint32_t c1 = c + nwaves;
-  uint32_t i1 = c1 * XE_WAVE + lane;
+  uint32_t i1 = chunk_base(P, c1, nchunks) + lane;
   bool v1 = c1 < nchunks && pkt_in_pass(P, i1);
   uint64_t r1lo, r1hi;  // raw descriptor of chunk c1, in flight
   desc_load(P, i1, v1, r1lo, r1hi);
@@ -2746,7 +2752,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     desc_fix(P, r1lo, r1hi, a1, l1);
     const bool f1 = hdr_issue(P, L.hdrbuf + (cur ^ 1u) * XE_HDR_BUF, a1, v1);
     const uint32_t c2 = c1 + nwaves;
-    const uint32_t i2 = c2 * XE_WAVE + lane;
+    const uint32_t i2 = chunk_base(P, c2, nchunks) + lane;
     const bool v2 = c2 < nchunks && pkt_in_pass(P, i2);
     desc_load(P, i2, v2, r1lo, r1hi);
     const uint32_t abort_flags = xe_load_relaxed32(P.flags);
@@ -2871,6 +2877,33 @@ XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t 
   for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w + 1 < K.kw ? en[1 + w] : 0;
   if (!hash_reserve(maps[m], kw)) xe_atomic_or32(K.err, 2u);
 }
+// D slot x, after the chains: the reservation of a new HASH key loses its "claimed in this launch" mark
+// (a chain's insert already turned it FULL; an unused one stays a plain tombstone holding its key), so a
+// later keyed batch's hash_reserve finds it by its key words instead of reserving another record
+XE_DEV void keyed_unnew_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x) {
+  if (!((XE_GP(const unsigned long long))K.dkid)[x]) return;
+  const uint64_t* en = K.dkey + uint64_t(x) * K.kw;
+  if (!(en[0] & XE_KEY_VALID) || (en[0] & 0x100ull)) return;
+  const XeDevMap& M = maps[uint32_t(en[0] & 0xffu)];
+  uint64_t kw[XE_MAX_KEY / 8];
+#pragma unroll
+  for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w + 1 < K.kw ? en[1 + w] : 0;
+  const uint32_t mask = M.cap - 1;
+  uint32_t idx = uint32_t(xe_hash_words(kw, M.kwords, M.key_size)) & mask;
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < M.cap; probe++) {
+    uint64_t* r = M.keys + uint64_t(idx) * M.rwords;
+    const uint32_t st = uint32_t(r[0]);
+    if (!(st & (XE_SLOT_FULL | XE_SLOT_TOMB))) return;  // the chain ends: nothing reserved for it
+    bool eq = true;
+    for (uint32_t k = 0; k < M.kwords; k++) eq = eq && r[1 + k] == kw[k];
+    if (eq) {
+      if (st & XE_SLOT_NEW) r[0] = (r[0] & ~uint64_t(XE_SLOT_NEW));
+      return;
+    }
+    idx = (idx + 1) & mask;
+  }
+}
 // chain lengths: a chain holding more than half the batch runs faster as the staged one-lane replay
 XE_DEV void keyed_cstart_item(const XeKeyed& K, uint32_t p) {
   if (p == 0 || K.okey[p] != K.okey[p - 1]) K.cstart[K.okey[p]] = p;
@@ -2890,6 +2923,7 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_RESERVE: keyed_reserve_item(K, maps, i); break;
     case XE_KS_CSTART: keyed_cstart_item(K, i); break;
     case XE_KS_CLONG: keyed_clong_item(K, i); break;
+    case XE_KS_UNNEW: keyed_unnew_item(K, maps, i); break;
     default: break;
   }
 }

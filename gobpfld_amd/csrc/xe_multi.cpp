@@ -206,9 +206,10 @@ int xe_run_batch_multi(xe_multi* m, void* const* d_umem, const uint64_t* umem_le
     // ---- in-order replay: shard k starts from the state shard k-1 ended with
     if (replayed) *replayed = 1;
     std::vector<uint64_t> sb(size_t(nmaps) + 1, 0);
-    for (int mi = 1; mi <= nmaps; mi++) xe_map_state_bytes(m->vms[0], mi, &sb[size_t(mi)]);
     auto transfer = [&](size_t from, size_t to) -> int {  // whole map state, VM `from` -> VM `to`
       for (int mi = 1; mi <= nmaps; mi++) {
+        // the exporter's image size (an ordered map's image follows its contents)
+        if (xe_map_state_bytes(m->vms[from], mi, &sb[size_t(mi)])) return -1;
         void* src = map_buf(from, mi, sb[size_t(mi)]);
         void* dst = map_buf(to, mi, sb[size_t(mi)]);
         if (!src || !dst || xe_map_state_export(m->vms[from], mi, src, nullptr)) return -1;

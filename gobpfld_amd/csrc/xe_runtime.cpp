@@ -41,6 +41,9 @@ extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDev
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_jit_may_write_entries(const XeUop* prog, size_t n);
+extern "C" size_t xe_jit_source_for(const XeUop* prog, size_t n, const XeDevMap* maps, uint32_t nmaps, int keyed,
+                                    char* buf, size_t buflen);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -651,6 +654,9 @@ struct xe_vm {
   bool jit_cyclic = false;
   bool jit_general = false;  // the per-program kernel uses the general lane model (loops, > 57 objects)
   std::string jit_error;
+  // its keyed variant (keyed ordered execution), built with it when the program may write map entries
+  void* kjit_fn = nullptr;
+  bool kjit_ready = false;
   Timer t0, t1, t2;
   // room the ordered maps' device copies keep for one run (elements / events, event bytes), grown
   // ×4 when a run reports XE_FLAG_CAPACITY
@@ -701,6 +707,7 @@ struct xe_vm {
   // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
   // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
   uint32_t keyed_backoff = 0;
+  uint32_t sched = 0;  // chunk -> wave schedule permutation of the parallel passes (xe_debug_set_schedule)
 };
 // ---- keyed ordered execution buffers (XeKeyed), sized for n packets
 static void keyed_free(xe_vm* vm) {
@@ -1653,6 +1660,7 @@ XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_
   P.rep = aux + 16;
   P.nrep = kRep;
   P.rep_words = 16 + 2 * (P.nmaps + 1);
+  P.sched = vm->sched;
   return P;
 }
 
@@ -1673,6 +1681,8 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
       vm->jit_nmaps = vm->maps.size();
+      vm->kjit_ready = false;
+      vm->kjit_fn = nullptr;
     }
     jit = vm->jit_fn;
     jit_general = vm->jit_general;
@@ -1685,6 +1695,38 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
   if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
 #endif
   return XE_OK;
+}
+
+// The keyed variant of the selected per-program kernel (null: the interpreter runs the keyed passes,
+// or the variant cannot be built). Built once per kernel, ahead of the batch that first needs it
+// (xe_prepare, or the start of a run whose program may write map entries), so no batch's device time
+// includes a compile.
+void* keyed_kernel(xe_vm* vm, void* jit) {
+#ifndef XE_HOSTSIM
+  if (!jit) return nullptr;
+  if (!vm->kjit_ready) {
+    const auto& prog = vm->programs[vm->entry];
+    bool cy = false, ge = false;
+    const char* jerr = "";
+    vm->kjit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
+                             uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
+    vm->kjit_ready = true;
+  }
+  return vm->kjit_fn;
+#else
+  (void)vm; (void)jit;
+  return nullptr;
+#endif
+}
+
+bool keyed_candidate(const xe_vm* vm) {
+#ifndef XE_HOSTSIM
+  const auto& prog = vm->programs[vm->entry];
+  return vm->settings.mode == XE_MODE_AUTO && xe_jit_may_write_entries(prog.data(), prog.size()) != 0;
+#else
+  (void)vm;
+  return false;
+#endif
 }
 
 // parallel-mode grid for the selected kernel (resident blocks; the general model's arena bounds it)
@@ -1901,17 +1943,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   // packets and records rolled back), 0 when done (used: XE_MODE_PARALLEL when no packet wrote a map
   // entry, so the SPEC pass was an ordinary parallel run; else XE_MODE_KEYED), < 0 on error.
   auto keyed = [&](uint32_t& used_out) -> int {
-    void* kjit = nullptr;
-#ifndef XE_HOSTSIM
-    if (jit) {  // the per-program kernel's keyed variant
-      const auto& prog = vm->programs[vm->entry];
-      bool cy = false, ge = false;
-      const char* jerr = "";
-      kjit = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
-                        uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
-      if (!kjit) return 1;
-    }
-#endif
+    void* kjit = keyed_kernel(vm, jit);  // the per-program kernel's keyed variant
+    if (jit && !kjit) return 1;
     auto klaunch = [&](const XeParams* p, uint32_t b) { return kjit ? launch_jit(kjit, p, b, 256, s) : launch_interp(p, b, 256, s); };
     // D table: 4x the last keyed batch's D keys (first time: n / 4), at most 2n (D holds <= n keys)
     uint32_t dmax = 4096, dcap = 4096;
@@ -2002,7 +2035,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     X.K.skip = nullptr;
     const uint32_t cgrid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (K.nO + 255) / 256));
     if (general && ensure_arena(vm, false, cgrid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
-    if (klaunch(&X, cgrid)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
+    if (klaunch(&X, cgrid) || step(XE_KS_UNNEW, K.dcap)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
     if (read_aux() || read_small()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
     if (run_conflict(red, P.nmaps)) return rollback(true) ? -1 : 1;  // a packet left its chain / an order-dependent add
     // the chains' inserts into the map counts
@@ -2021,6 +2054,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     return 0;
   };
 
+  if (jit && keyed_candidate(vm)) keyed_kernel(vm, jit);  // built before the timed region
   vm->t0.rec(s);
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
@@ -2160,6 +2194,41 @@ int complete_oldest(xe_vm* vm) {
 }
 
 }  // namespace
+
+// Build what the next batch runs, ahead of it: upload the maps, pick the engine and compile the
+// per-program kernel for the current program and map geometry (and its keyed variant when the program
+// may write map entries). Optional: the first batch does the same when this was not called.
+int xe_prepare(xe_vm* vm) {
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  if (int rc = prepare_run(vm, vm->stream)) return rc;
+  void* jit = nullptr;
+  bool jit_general = false;
+  if (int rc = select_engine(vm, jit, jit_general)) return rc;
+  if (jit && keyed_candidate(vm)) keyed_kernel(vm, jit);
+  return dsync(vm->stream) ? fail(vm, XE_ERR_DEVICE, "sync") : XE_OK;
+}
+
+// The generated source of the kernel xe_prepare would build (variant 0: the per-program kernel,
+// 1: its keyed variant), for a process that fills the kernel cache (xe_compile_kernel_source).
+int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len) {
+  if (!vm || (variant != 0 && variant != 1)) return XE_ERR_INVAL;
+#ifdef XE_HOSTSIM
+  (void)buf; (void)cap; (void)len;
+  return fail(vm, XE_ERR_UNSUPPORTED, "no per-program kernels in the host simulation");
+#else
+  if (int rc = xe_sync(vm)) return rc;
+  if (int rc = prepare_run(vm, vm->stream)) return rc;
+  if (vm->settings.engine == XE_ENGINE_INTERP || !jit_possible(vm))
+    return fail(vm, XE_ERR_UNSUPPORTED, "the program runs on the interpreter");
+  if (variant == 1 && !keyed_candidate(vm)) return fail(vm, XE_ERR_UNSUPPORTED, "no keyed variant for this program");
+  const auto& prog = vm->programs[vm->entry];
+  const size_t n = xe_jit_source_for(prog.data(), prog.size(), vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1),
+                                     variant, buf, cap);
+  if (len) *len = n;
+  return XE_OK;
+#endif
+}
 
 int xe_sync(xe_vm* vm) {
   if (!vm) return XE_ERR_INVAL;
@@ -2503,19 +2572,94 @@ int xe_shard_check(const uint64_t* fps, uint32_t ngpus, uint32_t nwords, uint32_
   return ok ? 1 : 0;
 }
 
+// Ordered maps (LRU_HASH, QUEUE, STACK, PERF_EVENT_ARRAY) keep their state in element pools and list
+// links, so their image is a serialisation of the host mirror in Go order (UsageList / Values /
+// Events), whose length follows the contents: [u64 magic][u64 records][u64 image bytes], then per
+// record {u32 nil_key, u32 key bytes, u32 value bytes, u32 0} and the key and value bytes, each padded
+// to 8. xe_map_state_bytes reports the current state's image size (the exporter's size is the one
+// the importer reads).
+}  // extern "C"
+namespace {
+constexpr uint64_t kOrdImageMagic = 0x78656f7264696d67ull;  // "xeordimg"
+uint64_t pad8(uint64_t v) { return (v + 7) & ~uint64_t(7); }
+uint64_t ordered_image_bytes(const HostMap& m) {
+  uint64_t b = 24;
+  for (const HostMap::Rec& r : m.items) b += 16 + pad8(r.key.size()) + pad8(r.val.size());
+  return b;
+}
+std::vector<uint8_t> ordered_image(const HostMap& m) {
+  std::vector<uint8_t> img(ordered_image_bytes(m), 0);
+  uint64_t hdr[3] = {kOrdImageMagic, m.items.size(), img.size()};
+  memcpy(img.data(), hdr, 24);
+  uint64_t at = 24;
+  for (const HostMap::Rec& r : m.items) {
+    const uint32_t rh[4] = {r.nil_key ? 1u : 0u, uint32_t(r.key.size()), uint32_t(r.val.size()), 0u};
+    memcpy(&img[at], rh, 16);
+    at += 16;
+    if (!r.key.empty()) memcpy(&img[at], r.key.data(), r.key.size());
+    at += pad8(r.key.size());
+    if (!r.val.empty()) memcpy(&img[at], r.val.data(), r.val.size());
+    at += pad8(r.val.size());
+  }
+  return img;
+}
+// the image of a map of the same geometry back into the host mirror; false when malformed
+bool ordered_from_image(HostMap& m, const std::vector<uint8_t>& img) {
+  if (img.size() < 24) return false;
+  uint64_t hdr[3];
+  memcpy(hdr, img.data(), 24);
+  if (hdr[0] != kOrdImageMagic || hdr[2] != img.size()) return false;
+  std::vector<HostMap::Rec> items;
+  uint64_t at = 24;
+  for (uint64_t i = 0; i < hdr[1]; i++) {
+    if (at + 16 > img.size()) return false;
+    uint32_t rh[4];
+    memcpy(rh, &img[at], 16);
+    at += 16;
+    if (at + pad8(rh[1]) + pad8(rh[2]) > img.size()) return false;
+    if ((m.dkind == XE_DM_LRU && !rh[0] && rh[1] != m.def.key_size) || (m.dkind != XE_DM_LRU && rh[1] != 0)) return false;
+    HostMap::Rec r;
+    r.nil_key = rh[0] != 0;
+    r.key.assign(img.begin() + long(at), img.begin() + long(at + rh[1]));
+    at += pad8(rh[1]);
+    r.val.assign(img.begin() + long(at), img.begin() + long(at + rh[2]));
+    at += pad8(rh[2]);
+    items.push_back(std::move(r));
+  }
+  if (at != img.size()) return false;
+  m.items = std::move(items);
+  return true;
+}
+}  // namespace
+extern "C" {
+
 int xe_map_state_bytes(xe_vm* vm, int32_t mi, uint64_t* bytes) {
   HostMap* m = get_map(vm, mi);
   if (!m || !bytes) return XE_ERR_INVAL;
+  if (m->ordered()) {
+    if (set_device(vm->settings.device) || map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+    *bytes = ordered_image_bytes(*m);
+    return XE_OK;
+  }
   *bytes = m->vals_alloc + (m->dkind == XE_DM_HASH ? uint64_t(m->cap + 1) * xe_hash_rwords(m->kwords) * 8 + 8 : 0);
   return XE_OK;
 }
 
-// [values][slot records][count u32, pad]: device-to-device copies on the VM's device
+// [values][slot records][count u32, pad]: device-to-device copies on the VM's device (ordered maps:
+// the serialised image above). Pipelined batches complete first (their replays rewrite the maps).
 int xe_map_state_export(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
   HostMap* m = get_map(vm, mi);
   if (!m || !d_out) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (m->ordered()) {
+    if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+    const std::vector<uint8_t> img = ordered_image(*m);
+    if (h2d(d_out, img.data(), img.size(), s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "state export");
+    return XE_OK;
+  }
   if (m->host_dirty && map_upload(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map upload");
   uint8_t* o = (uint8_t*)d_out;
   if (d2d(o, m->d_vals, m->vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "state export");
@@ -2529,11 +2673,25 @@ int xe_map_state_export(xe_vm* vm, int32_t mi, void* d_out, void* stream) {
 }
 
 int xe_map_state_import(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
-  if (vm) vm->staged_slot = -1;
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  vm->staged_slot = -1;
   HostMap* m = get_map(vm, mi);
   if (!m || !d_in) return XE_ERR_INVAL;
   set_device(vm->settings.device);
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
+  if (m->ordered()) {
+    uint64_t hdr[3] = {0, 0, 0};
+    if (d2h(hdr, d_in, 24, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "state import");
+    if (hdr[0] != kOrdImageMagic || hdr[2] < 24 || hdr[2] > (uint64_t(1) << 40))
+      return fail(vm, XE_ERR_INVAL, "state import: not an ordered-map image");
+    std::vector<uint8_t> img(hdr[2]);
+    if (d2h(img.data(), d_in, img.size(), s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "state import");
+    if (!ordered_from_image(*m, img)) return fail(vm, XE_ERR_INVAL, "state import: malformed ordered-map image");
+    m->host_dirty = true;  // the device copy is rebuilt from the mirror before the next run
+    m->dev_dirty = false;
+    return XE_OK;
+  }
   if (m->host_dirty && map_upload(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map upload");
   const uint8_t* in = (const uint8_t*)d_in;
   if (d2d(m->d_vals, in, m->vals_alloc, s) || d2d(m->d_snap, in, m->vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "state import");
@@ -2548,6 +2706,13 @@ int xe_map_state_import(xe_vm* vm, int32_t mi, const void* d_in, void* stream) {
   }
   if (dsync(s)) return fail(vm, XE_ERR_DEVICE, "state import");
   m->dev_dirty = true;
+  return XE_OK;
+}
+
+int xe_debug_set_schedule(xe_vm* vm, uint32_t sched) {
+  if (!vm) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  vm->sched = sched;
   return XE_OK;
 }
 

@@ -291,6 +291,32 @@ class VM:
         self._pending.append(pb)
         return pb
 
+    def prepare(self) -> None:
+        """xe_prepare: compile the per-program kernel (and its keyed variant) for the current program and
+        map geometry now instead of in the first batch. Releases the GIL (ctypes), so several VMs can
+        prepare from a thread pool and their kernels compile concurrently. No-op on libraries without it."""
+        if self.lib.has("prepare"):
+            self._check(self.lib.prepare(self.h), "prepare")
+
+    def kernel_sources(self) -> list[str]:
+        """Sources of the per-program kernels xe_prepare would build (the kernel, and its keyed variant
+        when the program may write map entries); [] when the VM runs the interpreter."""
+        out = []
+        for variant in (0, 1):
+            n = C.c_size_t()
+            rc = self.lib.kernel_source(self.h, variant, None, 0, C.byref(n))
+            if rc == -95:  # XE_ERR_UNSUPPORTED
+                continue
+            self._check(rc, "kernel source")
+            buf = C.create_string_buffer(n.value + 1)
+            self._check(self.lib.kernel_source(self.h, variant, buf, n.value + 1, C.byref(n)), "kernel source")
+            out.append(buf.value.decode())
+        return out
+
+    def set_schedule(self, sched: int) -> None:
+        """xe_debug_set_schedule: permute the chunk -> wave schedule of later parallel passes (0 = default)."""
+        self._check(self.lib.debug_set_schedule(self.h, sched), "set schedule")
+
     def sync(self) -> None:
         """Complete every pipelined batch (in-order replays included)."""
         rc = self.lib.sync(self.h)

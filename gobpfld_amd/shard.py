@@ -66,14 +66,17 @@ def _sum_deltas(vm, maps, dist, lanes, device, stream) -> None:
 
 
 def _mover(vm, maps, dist, device, stream):
-    """move(src, import_on): rank src's whole map state to the ranks import_on(rank) selects."""
+    """move(src, import_on): rank src's whole map state to the ranks import_on(rank) selects. The image
+    size is the source's (ordered maps serialise their current contents, so it varies): broadcast first."""
+    import torch
     rank = dist.get_rank()
-    sbytes = {m: vm.map_state_bytes(m) for m in maps}
-    sbufs = _bufs(vm, maps, device, "_shard_state_bufs", lambda m: sbytes[m])
 
     def move(src: int, import_on) -> None:
         for m in maps:
-            b = sbufs[m][: sbytes[m]]
+            size = torch.tensor([vm.map_state_bytes(m) if rank == src else 0], dtype=torch.int64, device=device)
+            dist.broadcast(size, src=src)
+            nb = int(size.item())
+            b = _bufs(vm, [m], device, "_shard_state_bufs", lambda _m: nb)[m][:nb]
             if rank == src:
                 vm.map_state_export(m, b.data_ptr(), stream=stream)
             dist.broadcast(b, src=src)

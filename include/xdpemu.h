@@ -261,6 +261,12 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
                               xe_batch_stats* stats);
 /* Complete every pipelined batch (replays included); returns the first error. */
 int xe_sync(xe_vm* vm);
+/* Build ahead of the next batch what it will run: map upload, engine choice and the per-program gfx950
+ * kernel for the current program and map geometry (plus its keyed-execution variant when the program
+ * may write map entries), so no batch pays a compile. Optional (the first batch does it otherwise); safe
+ * to call from several host threads on different VMs (their kernels compile concurrently).
+ * Not a reference entry point: the Go VM interprets (emulator/vm.go:110-173) and compiles nothing. */
+int xe_prepare(xe_vm* vm);
 /* Host-memory form (end-to-end: pinned staging + hipMemcpyAsync H2D/D2H). Packet writes made by the
  * program are copied back into umem (only when the program can write packet memory at all: a
  * may-point-to analysis of the program at load). results/regs may be NULL.
@@ -338,6 +344,23 @@ int xe_run_batch_multi(xe_multi* m, void* const* d_umem, const uint64_t* umem_le
                        const uint32_t* n, void* const* d_results, void* const* d_verdicts, xe_batch_stats* stats,
                        uint32_t* replayed);
 const char* xe_multi_last_error(const xe_multi* m);
+
+/* --- per-program kernel cache (no reference counterpart: the Go VM compiles nothing) ---
+ * A process-wide directory of compiled per-program kernels (code objects named by a hash of the
+ * generated source, the interpreter headers, the options and the gfx target); NULL/"" disables it.
+ * hiprtc compiles one kernel at a time per process, so a caller with many programs can have other
+ * processes fill the cache: xe_kernel_source gives the source xe_prepare would compile (variant 0: the
+ * per-program kernel, 1: its keyed-execution variant; XE_ERR_UNSUPPORTED when the VM runs none) and
+ * xe_compile_kernel_source compiles one into the directory without a device. NULL buf queries *len. */
+int xe_set_kernel_cache(const char* dir);
+int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len);
+int xe_compile_kernel_source(const char* src, const char* arch, const char* dir, char* err, size_t errlen);
+
+/* --- debug hooks (no reference counterpart) ---
+ * Permute the chunk -> wave schedule of the parallel passes (0 = the default walk; s > 0 = a fixed
+ * permutation of the 64-packet chunks). Results, register records and map contents may not depend on
+ * it: the determinism tests run one batch under several schedules and compare. */
+int xe_debug_set_schedule(xe_vm* vm, uint32_t sched);
 
 /* build / device info */
 const char* xe_version(void);

@@ -12,7 +12,8 @@ from gobpfld_amd import workloads as W
 from gobpfld_amd.emulator import VM, MapDef, Settings
 
 
-def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=None):
+def setup_one(lib, program, maps, settings=None, entries=None):
+    """A VM with `maps` (+ `entries`) and `program` (or a list: entrypoint first, tail-call targets after)."""
     vm = VM(settings or Settings(), lib=lib)
     idx = []
     for i, (mdef, init) in enumerate(maps):
@@ -28,11 +29,45 @@ def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=N
     progs = program if program and isinstance(program[0], list) else [program]
     p = [vm.add_raw_program(x) for x in progs][0]
     vm.set_entrypoint(p)
+    return vm, idx
+
+
+def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=None):
+    vm, idx = setup_one(lib, program, maps, settings, entries)
     mem = umem.copy()
     r = vm.run_batch(mem, descs, want_regs=regs)
     dumps = [_dump(vm, m) for m in idx]
     vm.close()
     return r, dumps, mem
+
+
+def precompile(lib, cases) -> int:
+    """Build the per-program kernels of many cases (program, maps, entries, settings) up front: each
+    case's VM is set up as run_one does, the sources of its kernels go to a pool of compile processes
+    that fill a kernel cache (gobpfld_amd/kcache.py; hiprtc compiles one kernel at a time per process),
+    and the tests that later run the cases one by one load their kernels from that cache. Cases the
+    per-program kernel cannot run contribute nothing. Returns the number of distinct kernels built."""
+    import tempfile
+    from gobpfld_amd import kcache
+    from gobpfld_amd.emulator import EmulatorError
+    if not lib.has("set_kernel_cache"):
+        return 0
+    d = getattr(precompile, "dir", None) or tempfile.mkdtemp(prefix="xe-kernels-")
+    precompile.dir = kcache.enable(lib, d)
+    sources = []
+    for program, maps, entries, settings in cases:
+        try:
+            vm = setup_one(lib, program, maps, settings, entries)[0]
+        except EmulatorError:
+            continue
+        try:
+            sources += vm.kernel_sources()
+        except EmulatorError:
+            pass
+        vm.close()
+    uniq = list(dict.fromkeys(sources))
+    kcache.fill(uniq, d)
+    return len(uniq)
 
 
 def _dump(vm, m):

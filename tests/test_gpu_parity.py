@@ -10,11 +10,29 @@ import pytest
 from gobpfld_amd import workloads as W
 from gobpfld_amd.emulator import EmulatorError, ENGINE_INTERP, ENGINE_JIT, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
 from kats import KATS
-from parity import assert_same, config_case, packets, run_one
+from parity import assert_same, config_case, packets, precompile, run_one
 
 pytestmark = pytest.mark.gpu
 ENGINES = [ENGINE_INTERP, ENGINE_JIT]
 ENGINE_IDS = ["interp", "jit"]
+FUZZ_COUNTS = {ENGINE_INTERP: 240, ENGINE_JIT: 48}
+CONFIGS = [("c1", 1024, None), ("c2", 65536, None), ("c3", 30000, 8192), ("c4", 8192, None), ("c5", 30000, 8192)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _kernels_built(gpu_lib):
+    """Every per-program kernel this module runs, built up front in parallel (xe_prepare in a thread
+    pool): the KATs, the reduced configs and the fuzz programs on the JIT engine."""
+    from fuzz import gen_program
+    cases = [(k["program"], k["maps"], k["entries"], Settings(engine=ENGINE_JIT)) for k in KATS]
+    for name, n, cap in CONFIGS:
+        prog, maps, entries, _, _ = config_case(name, 16, cap)
+        cases.append((prog, maps, entries, Settings(engine=ENGINE_JIT)))
+    for seed in range(FUZZ_COUNTS[ENGINE_JIT]):
+        prog, maps, entries, settings = gen_program(seed, 24 + seed % 64)
+        settings.engine = ENGINE_JIT
+        cases.append((prog, maps, entries, settings))
+    precompile(gpu_lib, cases)
 
 
 @pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
@@ -33,8 +51,7 @@ def test_kat_device_equals_oracle(gpu_lib, oracle_lib, k, engine):
 
 
 @pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
-@pytest.mark.parametrize("name,n,cap", [("c1", 1024, None), ("c2", 65536, None), ("c3", 30000, 8192),
-                                        ("c4", 8192, None), ("c5", 30000, 8192)])
+@pytest.mark.parametrize("name,n,cap", CONFIGS)
 def test_config_device_equals_oracle(gpu_lib, oracle_lib, name, n, cap, engine):
     prog, maps, entries, umem, descs = config_case(name, n, cap)
     a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=Settings(engine=engine))
@@ -129,7 +146,7 @@ def test_c2_full_size_properties(gpu_lib):
     vm.close()
 
 
-@pytest.mark.parametrize("engine,count", [(ENGINE_INTERP, 240), (ENGINE_JIT, 48)], ids=ENGINE_IDS)
+@pytest.mark.parametrize("engine,count", list(FUZZ_COUNTS.items()), ids=ENGINE_IDS)
 def test_fuzz_device_equals_oracle(gpu_lib, oracle_lib, engine, count):
     """Random programs (tests/fuzz.py): device == oracle on every observable, per engine."""
     from fuzz import gen_program

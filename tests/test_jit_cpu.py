@@ -63,3 +63,25 @@ def test_generated_source_shape(prod):
     assert "#define XE_REGS_FIELDS" in src and "xe_jit_kernel" in src
     assert src.count("\nL") >= n            # one labelled block per instruction slot
     assert "steps >= P.max_steps" not in src.split("XE_DEV void xe_jit_body")[1].split("L0:")[1].split("L1:")[0]
+
+
+def test_kernel_cache_fill(prod, tmp_path):
+    """gobpfld_amd/kcache.py: worker processes compile generated sources into the on-disk kernel cache
+    (xe_compile_kernel_source, no device); one object per distinct source, named by the content hash
+    (a changed source gets a new object), and a second fill finds everything cached."""
+    from gobpfld_amd import kcache
+    srcs = []
+    for name in ("c1", "c2", "c4"):
+        u, n = _uops(prod, W.CONFIGS[name]["program"]())
+        buf = C.create_string_buffer(1 << 21)
+        prod.xe_jit_source(u.ctypes.data, n, buf, 1 << 21)
+        srcs.append(buf.value.decode())
+    srcs.append(srcs[0])                                      # duplicates compile once
+    assert kcache.fill(srcs, tmp_path, workers=3) == []
+    objs = sorted(p.name for p in tmp_path.glob("xe_*.co"))
+    assert len(objs) == 3 and all(len(p) == len("xe_") + 32 + len(".co") for p in objs)
+    mtimes = {p.name: p.stat().st_mtime_ns for p in tmp_path.glob("xe_*.co")}
+    assert kcache.fill(srcs[:1] + [srcs[1] + "\n// changed\n"], tmp_path, workers=2) == []
+    after = {p.name: p.stat().st_mtime_ns for p in tmp_path.glob("xe_*.co")}
+    assert len(after) == 4 and all(after[k] == v for k, v in mtimes.items())
+    assert kcache.fill(["this is not HIP"], tmp_path, workers=1)   # a compile error is reported

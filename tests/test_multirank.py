@@ -18,7 +18,7 @@ from gobpfld_amd import workloads as W
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [("c2", 8192, None, True), ("c5", 8192, 4096, True), ("u32wrap", 64, None, True),
          ("mixedwrap", 64, None, False), ("readvsadd", 256, None, False), ("addvsread", 256, None, True),
-         ("rmw", 256, None, False)]
+         ("rmw", 256, None, False), ("lru", 512, None, False), ("queue", 512, None, False)]
 # shard epochs (several batches per exchange): a read of a field any other rank adds to needs the
 # replay, so addvsread (rank 0 reads what rank 1 adds) no longer commutes
 EPOCH_CASES = [c if c[0] != "addvsread" else (c[0], c[1], c[2], False) for c in CASES]
@@ -42,7 +42,7 @@ def _batch(name, start, n):
         second = np.arange(start, start + n) >= _batch.total // 2
         umem[::64] = np.where(second != (name == "addvsread"), 255, 0)
         return umem, descs
-    return W.build_batch("c2" if name in ("u32wrap", "mixedwrap") else name, start, n)
+    return W.build_batch("c2" if name in ("u32wrap", "mixedwrap", "lru", "queue") else name, start, n)
 
 
 _batch.total = 256
@@ -78,11 +78,39 @@ def _rank(rank, world, port, name, n, cap, out_dir):
 
 
 def _dump(vm, m):
+    from gobpfld_amd.emulator import MAP_LRU_HASH
     d = vm.map_dump(m)
     if isinstance(d, bytes):
         return d
+    if isinstance(d, list):  # QUEUE / STACK / PERF records in list order
+        return b"|".join(d) + b"#" + str(len(d)).encode()
     keys, vals = d
-    return np.asarray(keys).tobytes() + b"|" + np.asarray(vals).tobytes()
+    out = np.asarray(keys).tobytes() + b"|" + np.asarray(vals).tobytes()
+    if vm.map_defs[m].type == MAP_LRU_HASH:
+        out += b"|" + b"".join(vm.map_lru_order(m))
+    return out
+
+
+def _ordered_program(queue: bool):
+    """Ordered maps (order-dependent by nature, so the shards always replay in order through the
+    whole-state exchange of ordered maps). lru: LRU_HASH(4 entries) keyed by byte 0 & 7 — a hit returns
+    the stored byte, a miss inserts byte 1 (evicting the least recently used key). queue: push byte 0
+    onto a QUEUE (bpf_map_push_elem) and return byte 0."""
+    from gobpfld_amd.asm import JEQ, Asm
+    a = Asm()
+    a.ldx(4, 6, 1, 0).ldx(1, 8, 6, 0)
+    if queue:
+        a.stx(8, 10, -8, 8).ld_map(1, 1).mov64(2, src=10).add64(2, -8).mov64(3, 0).call(87)
+        a.mov64(0, src=8).exit()
+        return a.assemble()
+    a.alu64(0x50, 8, 7).stx(4, 10, -4, 8).ldx(1, 9, 6, 1).stx(8, 10, -16, 9)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "miss", imm=0)
+    a.ldx(8, 0, 0, 0).exit()
+    a.label("miss")
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4).mov64(3, src=10).add64(3, -16).mov64(4, 0).call(2)
+    a.mov64(0, 2).exit()
+    return a.assemble()
 
 
 def _wrap_program(mixed: bool):
@@ -119,7 +147,11 @@ def _role_program(rmw: bool):
 
 
 def _setup(vm, name, cap):
-    from gobpfld_amd.emulator import MAP_ARRAY, MapDef
+    from gobpfld_amd.emulator import MAP_ARRAY, MAP_LRU_HASH, MAP_QUEUE, MapDef
+    if name in ("lru", "queue"):
+        vm.add_map(MapDef(MAP_QUEUE, 0, 8, 1 << 16) if name == "queue" else MapDef(MAP_LRU_HASH, 4, 8, 4))
+        vm.set_entrypoint(vm.add_raw_program(_ordered_program(name == "queue")))
+        return
     if name in ("u32wrap", "mixedwrap"):
         vm.add_map(MapDef(MAP_ARRAY, 4, 8, 4), {0: (0xFFF0FFFFFFF0).to_bytes(8, "little")})
         vm.set_entrypoint(vm.add_raw_program(_wrap_program(name == "mixedwrap")))

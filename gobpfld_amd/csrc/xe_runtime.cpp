@@ -36,14 +36,14 @@ extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, cons
 extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s);
 extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* scratch_bytes,
                                       uint32_t* flag, hipStream_t s);
-extern "C" void* xe_jit_get(const XeUop* prog, size_t n, int device, const XeDevMap* maps, uint32_t nmaps, bool* cyclic,
-                            bool* general, const char** err, int keyed);
+extern "C" void* xe_jit_get(const XeUop* const* progs, const uint32_t* lens, uint32_t nprogs, int32_t entry, int device,
+                            const XeDevMap* maps, uint32_t nmaps, bool* cyclic, bool* general, const char** err, int keyed);
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_jit_may_write_entries(const XeUop* prog, size_t n);
-extern "C" size_t xe_jit_source_for(const XeUop* prog, size_t n, const XeDevMap* maps, uint32_t nmaps, int keyed,
-                                    char* buf, size_t buflen);
+extern "C" size_t xe_jit_source_for(const XeUop* const* progs, const uint32_t* lens, uint32_t nprogs, int32_t entry,
+                                    const XeDevMap* maps, uint32_t nmaps, int keyed, char* buf, size_t buflen);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -650,6 +650,7 @@ struct xe_vm {
   // per-program kernel (JIT engine) for the current entry program
   int32_t jit_idx = -1;
   size_t jit_nmaps = 0;
+  size_t jit_nprogs = 0;  // programs of the VM when the kernel was built (tail calls compile them all in)
   void* jit_fn = nullptr;
   bool jit_cyclic = false;
   bool jit_general = false;  // the per-program kernel uses the general lane model (loops, > 57 objects)
@@ -1582,17 +1583,25 @@ static bool may_write_packet(const std::vector<XeUop>& prog) {
   return true;
 }
 
-// Can the program run as a per-program kernel? Not with bpf-to-bpf calls or tail calls (the frames,
-// clones and program switches live in the interpreter's general model), the ordered maps, or helpers
-// whose id is only known at run time.
-static bool jit_possible(const xe_vm* vm) {
-  for (const XeUop& u : vm->programs[vm->entry]) {
-    if (u.cls == U_CALLBPF || u.cls == U_CALLX) return false;
-    if (u.cls == U_HELPER && (u.imm == 12 || u.imm == 25 || u.imm == 87 || u.imm == 88 || u.imm == 89)) return false;
+// Can the program run as a per-program kernel? Every program can: bpf-to-bpf calls, tail calls (every
+// program of the VM compiled in), indirect helper calls and the ordered maps take the kernel's dynamic
+// form over the general lane model (xe_jit.cpp generate_dynamic).
+static bool jit_possible(const xe_vm* vm) { return vm->entry >= 1 && vm->entry < int32_t(vm->programs.size()); }
+
+// the VM's programs as pointer / length tables (index 0 unused) for the kernel generator
+struct ProgTab {
+  std::vector<const XeUop*> p;
+  std::vector<uint32_t> n;
+};
+static ProgTab prog_tab(const xe_vm* vm) {
+  ProgTab t;
+  t.p.assign(vm->programs.size(), nullptr);
+  t.n.assign(vm->programs.size(), 0);
+  for (size_t q = 1; q < vm->programs.size(); q++) {
+    t.p[q] = vm->programs[q].data();
+    t.n[q] = uint32_t(vm->programs[q].size());
   }
-  for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].ordered()) return false;
-  return true;
+  return t;
 }
 static bool has_callbpf(const xe_vm* vm) {
   for (size_t p = 1; p < vm->programs.size(); p++)
@@ -1672,15 +1681,17 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
 #ifndef XE_HOSTSIM
   const uint32_t engine = vm->settings.engine;
   if (engine != XE_ENGINE_INTERP && jit_possible(vm)) {
-    if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size()) {
+    if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size() || vm->jit_nprogs != vm->programs.size()) {
       // the kernel is specialised on the program and the map geometry (xe_jit.cpp)
-      const auto& prog = vm->programs[vm->entry];
+      const ProgTab t = prog_tab(vm);
       const char* jerr = "";
-      vm->jit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
-                              uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic, &vm->jit_general, &jerr, 0);
+      vm->jit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
+                              vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic,
+                              &vm->jit_general, &jerr, 0);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
       vm->jit_nmaps = vm->maps.size();
+      vm->jit_nprogs = vm->programs.size();
       vm->kjit_ready = false;
       vm->kjit_fn = nullptr;
     }
@@ -1688,9 +1699,6 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
     jit_general = vm->jit_general;
     // acyclic kernels carry no budget checks: exact only while the budget cannot be reached
     if (jit && !vm->jit_cyclic && vm->settings.max_steps < vm->d_prog_len) jit = nullptr;
-  } else if (engine == XE_ENGINE_JIT) {
-    vm->jit_error = "the program needs the interpreter's general model (bpf-to-bpf or tail calls, ordered maps, "
-                    "indirect helper calls)";
   }
   if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
 #endif
@@ -1705,11 +1713,11 @@ void* keyed_kernel(xe_vm* vm, void* jit) {
 #ifndef XE_HOSTSIM
   if (!jit) return nullptr;
   if (!vm->kjit_ready) {
-    const auto& prog = vm->programs[vm->entry];
+    const ProgTab t = prog_tab(vm);
     bool cy = false, ge = false;
     const char* jerr = "";
-    vm->kjit_fn = xe_jit_get(prog.data(), prog.size(), vm->settings.device, vm->dm_uploaded.data(),
-                             uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
+    vm->kjit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
+                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
     vm->kjit_ready = true;
   }
   return vm->kjit_fn;
@@ -2222,13 +2230,22 @@ int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len)
   if (vm->settings.engine == XE_ENGINE_INTERP || !jit_possible(vm))
     return fail(vm, XE_ERR_UNSUPPORTED, "the program runs on the interpreter");
   if (variant == 1 && !keyed_candidate(vm)) return fail(vm, XE_ERR_UNSUPPORTED, "no keyed variant for this program");
-  const auto& prog = vm->programs[vm->entry];
-  const size_t n = xe_jit_source_for(prog.data(), prog.size(), vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1),
-                                     variant, buf, cap);
+  const ProgTab t = prog_tab(vm);
+  const size_t n = xe_jit_source_for(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry,
+                                     vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), variant, buf, cap);
   if (len) *len = n;
   return XE_OK;
 #endif
 }
+
+#ifdef XE_HOSTSIM
+// the host simulation builds no per-program kernels (xe_jit.cpp is not part of it)
+int xe_set_kernel_cache(const char*) { return XE_OK; }
+int xe_compile_kernel_source(const char*, const char*, const char*, char* err, size_t errlen) {
+  if (err && errlen) err[0] = 0;
+  return XE_ERR_UNSUPPORTED;
+}
+#endif
 
 int xe_sync(xe_vm* vm) {
   if (!vm) return XE_ERR_INVAL;

@@ -404,21 +404,32 @@ int translate(const uint64_t* raw, uint32_t n, std::vector<XeUop>& out, std::str
 // store changes map memory exactly as an atomic add of +-K (mod 2^width) would: the only thing the
 // lane keeps from the loaded value is the stored sum. Marking the pair UF_LIFT lets a parallel lane
 // skip the read footprint and add instead of store (uop_ldx / uop_store), so `value->count++` written
-// without an atomic runs in parallel instead of conflicting into the ordered replay. Programs with
-// bpf-to-bpf calls, tail calls or indirect helper calls are left alone (their register flow leaves the
-// program's own CFG). The stx carries the addend: imm = K, x = (rY + 1 or 0) | 0x100 when subtracting.
+// without an atomic runs in parallel instead of conflicting into the ordered replay. Programs with tail
+// calls or indirect helper calls are left alone (their register flow leaves the program). bpf-to-bpf
+// calls are followed: a call flows into its callee and, when the callee returns, on to the next slot
+// (emulator/inst_call_bpf.go:18-44, inst_exit.go:22-48). The call keeps R6..R9 (it clones them for the
+// return), an Exit returns R0..R5 to whichever call site is live. The stx carries the addend:
+// imm = K, x = (rY + 1 or 0) | 0x100 when subtracting.
 void lift_rmw(std::vector<XeUop>& p) {
   const size_t n = p.size();
   for (const XeUop& u : p)
-    if (u.cls == U_CALLBPF || u.cls == U_CALLX || (u.cls == U_HELPER && u.imm == 12)) return;
+    if (u.cls == U_CALLX || (u.cls == U_HELPER && u.imm == 12)) return;
   std::vector<bool> target(n + 1, false);
-  for (const XeUop& u : p)
-    if ((u.cls == U_JA || u.cls == U_JMP) && int64_t(u.tgt) + 1 >= 0 && size_t(int64_t(u.tgt) + 1) <= n) target[size_t(u.tgt + 1)] = true;
-  // backward liveness over R0..R10 (bit r); exit reads R0, helpers read R1..R5 and define nothing
+  auto mark = [&](int64_t t) { if (t >= 0 && size_t(t) <= n) target[size_t(t)] = true; };
+  for (size_t k = 0; k < n; k++) {
+    const XeUop& u = p[k];
+    if (u.cls == U_JA || u.cls == U_JMP) mark(int64_t(u.tgt) + 1);
+    if (u.cls == U_CALLBPF) { mark(int64_t(k) + u.imm + 1); mark(int64_t(k) + 1); }
+  }
+  // backward liveness over R0..R10 (bit r); exit reads R0 (and, inside a call, what the return sites
+  // read of R0..R5), helpers read R1..R5 and define nothing
   std::vector<uint16_t> live(n + 1, 0);
   auto bit = [](int r) { return uint16_t(r >= 0 && r <= 10 ? 1u << r : 0u); };
+  uint16_t ret_live = 0;
   for (bool changed = true; changed;) {
     changed = false;
+    for (size_t k = 0; k < n; k++)
+      if (p[k].cls == U_CALLBPF && k + 1 < n && (live[k + 1] & 0x3f & ~ret_live)) { ret_live |= live[k + 1] & 0x3f; changed = true; }
     for (size_t k = n; k-- > 0;) {
       const XeUop& u = p[k];
       auto at = [&](int64_t t) -> uint16_t { return t >= 0 && size_t(t) < n ? live[size_t(t)] : 0; };
@@ -427,10 +438,12 @@ void lift_rmw(std::vector<XeUop>& p) {
         case U_EXIT: case U_FAIL: break;
         case U_JA: out = at(int64_t(u.tgt) + 1); break;
         case U_JMP: out = uint16_t(at(int64_t(u.tgt) + 1) | at(int64_t(k) + 1)); break;
+        case U_CALLBPF: out = uint16_t(at(int64_t(k) + u.imm + 1) | at(int64_t(k) + 1)); break;
         default: out = at(int64_t(k) + 1); break;
       }
       switch (u.cls) {
-        case U_EXIT: use = bit(0); break;
+        case U_EXIT: use = uint16_t(bit(0) | ret_live); break;
+        case U_CALLBPF: use = 0x3c0; break;  // R6..R9 are cloned for the return
         case U_ALU: use = uint16_t(bit(u.dst) | ((u.fl & UF_REG) ? bit(u.src) : 0)); def = bit(u.dst); break;
         case U_MOVI: case U_LDIMM64: def = bit(u.dst); break;
         case U_MOVR: use = bit(u.src); def = bit(u.dst); break;

@@ -22,10 +22,18 @@ _worker_lib = None
 
 def _worker_init(lib_path: str) -> None:
     global _worker_lib
-    # comgr's own code cache (~/.cache/comgr) is not safe for concurrent writers: two compiling
-    # processes sharing it die of SIGBUS (a file mapped by one is rewritten by the other). The workers
-    # fill our cache anyway, so theirs is off.
+    import atexit
+    import shutil
+    import tempfile
+    # Concurrent hiprtc processes must not share comgr's scratch space: with a common TMPDIR their
+    # temporary files collide (workers died of SIGBUS / hung after a few compiles), and comgr's own code
+    # cache (~/.cache/comgr) is not safe for concurrent writers either. Each worker gets a private
+    # scratch directory and no comgr cache (it fills ours).
+    scratch = tempfile.mkdtemp(prefix="xe-kc-")
+    os.environ["TMPDIR"] = scratch
     os.environ["AMD_COMGR_CACHE"] = "0"
+    tempfile.tempdir = scratch
+    atexit.register(shutil.rmtree, scratch, True)
     _worker_lib = C.CDLL(lib_path)
     fn = _worker_lib.xe_compile_kernel_source
     fn.restype = C.c_int

@@ -262,6 +262,63 @@ def prog_c5() -> list[int]:
     return a.assemble()
 
 
+def prog_bpf2bpf() -> list[int]:
+    """Call-heavy analogue of the reference's cmd/examples/bpf_to_bpf/src/xdp.c: the XDP section parses
+    Ethernet / IPv4 and calls a non-inlined sub-program (bpf-to-bpf, emulator/inst_call_bpf.go:18-44)
+    once for the IP protocol's stats and once more for the TCP or UDP destination port's stats. The
+    sub-program looks the key up and either bumps {pkts, bytes} with plain loads / stores (the C
+    `stats_ptr->pkts++`, lifted to adds) or inserts a fresh {1, framesize} (bpf_map_update_elem).
+    HASH maps instead of the example's LRU_PERCPU_HASH (the same helper calls). Maps: 1 protocols,
+    2 TCP ports, 3 UDP ports (4-byte keys, {u64 pkts, u64 bytes})."""
+    a = Asm()
+    a.ldx(4, 6, 1, 0).ldx(4, 7, 1, 4)
+    a.mov64(2, src=6).add64(2, 14)
+    a.jmp(JGT, 2, "pass", src=7)
+    a.ldx(2, 3, 6, 12)
+    a.jmp(JNE, 3, "pass", imm=0x0008)
+    a.mov64(9, src=6).add64(9, 14)
+    a.mov64(5, src=9).add64(5, 24)
+    a.jmp(JGT, 5, "pass", src=7)
+    a.ldx(2, 8, 9, 2).end(8, 16, to_be=False)  # framesize = ntohs(ip->tot_len) (to_le swaps, A10)
+    a.ld_map(1, 1).ldx(1, 2, 9, 9).mov64(3, src=8)
+    a.call_bpf("inc")                          # inc_ip_proto(proto, framesize)
+    a.ldx(1, 2, 9, 9)
+    a.jmp(JEQ, 2, "tcp", imm=6)
+    a.jmp(JNE, 2, "pass", imm=17)
+    a.ld_map(1, 3).ja("port")
+    a.label("tcp").ld_map(1, 2)
+    a.label("port").ldx(2, 2, 9, 22).end(2, 16, to_be=False)  # le_dest = ntohs(dest)
+    a.mov64(3, src=8)
+    a.call_bpf("inc")                          # inc_tcp / inc_udp(dest, framesize)
+    a.label("pass").mov64(0, XDP_PASS).exit()
+    # inc(map r1, key r2, framesize r3): lookup; hit: pkts++, bytes += framesize; miss: insert {1, size}
+    a.label("inc")
+    a.mov64(6, src=1).mov64(7, src=3)
+    a.stx(4, 10, -8, 2)
+    a.mov64(2, src=10).add64(2, -8).call(1)
+    a.jmp(JEQ, 0, "new", imm=0)
+    a.ldx(8, 1, 0, 0).add64(1, 1).stx(8, 0, 0, 1)
+    a.ldx(8, 1, 0, 8).add64(1, src=7).stx(8, 0, 8, 1)
+    a.mov64(0, 0).exit()
+    a.label("new")
+    a.st(8, 10, -24, 1).stx(8, 10, -16, 7)
+    a.mov64(1, src=6).mov64(2, src=10).add64(2, -8).mov64(3, src=10).add64(3, -24).mov64(4, 0).call(2)
+    a.mov64(0, 0).exit()
+    return a.assemble()
+
+
+BPF2BPF_PORTS = 1 << 14   # the C5 stream's destination ports (flow_tuples: 14 bits)
+
+
+def bpf2bpf_map_entries() -> list[tuple[np.ndarray, np.ndarray]]:
+    """Every key the stream uses preloaded (protocols 0..255, ports 0..16383): no inserts, so the batch
+    stays commutative (lifted adds)."""
+    protos = np.arange(256, dtype=np.uint32).view(np.uint8).reshape(-1, 4)
+    ports = np.arange(BPF2BPF_PORTS, dtype=np.uint32).view(np.uint8).reshape(-1, 4)
+    return [(protos, np.zeros((256, 16), np.uint8)), (ports, np.zeros((BPF2BPF_PORTS, 16), np.uint8)),
+            (ports.copy(), np.zeros((BPF2BPF_PORTS, 16), np.uint8))]
+
+
 # ----------------------------------------------------------------------------- packets
 ETH_IPV4 = 0x0800
 ETH_IPV6 = 0x86DD
@@ -430,6 +487,14 @@ def headers_c5(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
     return _ipv4_l4_headers(5, idx, flow_tuples(5, fid), hdr)
 
 
+def headers_bpf2bpf(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
+    """C5's stream with the IPv4 total length filled in (64-byte frames: 50), the framesize the
+    call-heavy program accounts."""
+    h = headers_c5(idx, hdr)
+    h[:, 16], h[:, 17] = 0, 50
+    return h
+
+
 def c3_map_entries() -> tuple[np.ndarray, np.ndarray]:
     fid = np.arange(C3_FLOWS, dtype=np.uint64)
     keys = key_from_tuple(flow_tuples(3, fid))
@@ -452,6 +517,7 @@ CONFIGS = {
     "c3learn": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
     "c4": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024),
     "c5": dict(program=prog_c5, pkt=64, n=256 * 1024 * 1024),
+    "bpf2bpf": dict(program=prog_bpf2bpf, pkt=64, n=4 * 1024 * 1024),
 }
 
 
@@ -462,6 +528,10 @@ def workload_maps(name: str) -> list[tuple[MapDef, tuple[np.ndarray, np.ndarray]
         return [(MapDef(MAP_HASH, 16, 16, C3_MAX), c3_map_entries())]
     if name == "c5":
         return [(MapDef(MAP_HASH, 16, 16, C5_MAX), c5_map_entries())]
+    if name == "bpf2bpf":
+        e = bpf2bpf_map_entries()
+        return [(MapDef(MAP_HASH, 4, 16, 256), e[0]), (MapDef(MAP_HASH, 4, 16, BPF2BPF_PORTS), e[1]),
+                (MapDef(MAP_HASH, 4, 16, BPF2BPF_PORTS), e[2])]
     return []
 
 
@@ -473,7 +543,7 @@ def headers(name: str, idx: np.ndarray, hdr: int = 64) -> np.ndarray:
             h[:, b] = (r >> np.uint64(8 * (b % 8))) & np.uint64(0xFF)
         return h
     return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c4": headers_c4,
-            "c5": headers_c5}[name](idx, hdr)
+            "c5": headers_c5, "bpf2bpf": headers_bpf2bpf}[name](idx, hdr)
 
 
 def packet_sizes(name: str, idx: np.ndarray) -> np.ndarray:

@@ -39,3 +39,32 @@ def gpu_lib(built):
         pytest.fail("GPU test selected but no GPU is visible")
     from gobpfld_amd import _native as N
     return N.product()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _kernel_cache(request):
+    """GPU sessions: build every per-program kernel the suite uses in worker processes, in the
+    background, into a session kernel cache (gobpfld_amd/kcache.py; hiprtc compiles one kernel at a time
+    per process). Tests start at once and load their kernels from the cache when it has them; a test
+    that gets there first compiles its own, exactly as without the cache."""
+    if not any(item.get_closest_marker("gpu") for item in request.session.items):
+        yield None
+        return
+    import tempfile
+    import threading
+    import torch
+    if not torch.cuda.is_available():
+        yield None
+        return
+    from gobpfld_amd import _native as N
+    from gobpfld_amd import build as B
+    from gobpfld_amd import kcache
+    from kernel_cases import gpu_cases
+    from parity import kernel_sources
+    B.build_all()
+    lib = N.product()
+    d = kcache.enable(lib, tempfile.mkdtemp(prefix="xe-kernels-"))
+    sources = kernel_sources(lib, gpu_cases())
+    t = threading.Thread(target=kcache.fill, args=(sources, d), daemon=True)
+    t.start()
+    yield d

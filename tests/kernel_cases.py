@@ -1,0 +1,35 @@
+"""The per-program kernels the -m gpu suite builds, listed once so a session can build them all up front
+in worker processes (gobpfld_amd/kcache.py) while the first tests run; each test's own build then finds
+its kernel in the cache (or compiles it itself if it is not there yet: the cache only saves time)."""
+from __future__ import annotations
+
+from gobpfld_amd.emulator import MAP_ARRAY, MAP_HASH, MapDef, Settings
+
+JIT = 2
+
+
+def gpu_cases():
+    """(program, maps, entries, settings) in roughly the order the suite reaches them."""
+    from fuzz import gen_program
+    from kats import KATS
+    from parity import config_case
+    cases = []
+    for name, cap in (("c1", None), ("c2", None), ("c3", 8192), ("c4", None), ("c5", 8192), ("bpf2bpf", None)):
+        prog, maps, entries, _, _ = config_case(name, 16, cap)
+        cases.append((prog, maps, entries, Settings(engine=JIT)))
+    cases += [(k["program"], k["maps"], k["entries"], Settings(engine=JIT)) for k in KATS]
+    for seed in range(48):
+        prog, maps, entries, settings = gen_program(seed, 24 + seed % 64)
+        settings.engine = JIT
+        cases.append((prog, maps, entries, settings))
+    import test_keyed as K
+    for c in sorted(K.CASES):
+        cases.append((*K.CASES[c](), Settings(engine=JIT)))
+    prog, maps, entries, _, _ = config_case("c3learn", 16)
+    cases.append((prog, maps, entries, Settings(engine=JIT)))
+    cases.append((K.prog_escape(), [(MapDef(MAP_HASH, 4, 8, 64), None), (MapDef(MAP_ARRAY, 4, 8, 8), None)], None,
+                  Settings(engine=JIT)))
+    cases.append((K.prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, Settings()))
+    cases.append((K.prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, Settings()))
+    cases.append((K.prog_first_seen(), [(MapDef(MAP_HASH, 4, 8, 256), None)], None, Settings()))
+    return cases

@@ -41,19 +41,10 @@ def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=N
     return r, dumps, mem
 
 
-def precompile(lib, cases) -> int:
-    """Build the per-program kernels of many cases (program, maps, entries, settings) up front: each
-    case's VM is set up as run_one does, the sources of its kernels go to a pool of compile processes
-    that fill a kernel cache (gobpfld_amd/kcache.py; hiprtc compiles one kernel at a time per process),
-    and the tests that later run the cases one by one load their kernels from that cache. Cases the
-    per-program kernel cannot run contribute nothing. Returns the number of distinct kernels built."""
-    import tempfile
-    from gobpfld_amd import kcache
+def kernel_sources(lib, cases) -> list[str]:
+    """Sources of the per-program kernels of many cases (program, maps, entries, settings), each case's
+    VM set up as run_one does (xe_kernel_source); cases that run on the interpreter contribute none."""
     from gobpfld_amd.emulator import EmulatorError
-    if not lib.has("set_kernel_cache"):
-        return 0
-    d = getattr(precompile, "dir", None) or tempfile.mkdtemp(prefix="xe-kernels-")
-    precompile.dir = kcache.enable(lib, d)
     sources = []
     for program, maps, entries, settings in cases:
         try:
@@ -65,7 +56,20 @@ def precompile(lib, cases) -> int:
         except EmulatorError:
             pass
         vm.close()
-    uniq = list(dict.fromkeys(sources))
+    return list(dict.fromkeys(sources))
+
+
+def precompile(lib, cases) -> int:
+    """Build the per-program kernels of `cases` into the session's kernel cache now (worker processes,
+    gobpfld_amd/kcache.py): the tests that run the cases one by one then load them. Returns the number of
+    distinct kernels."""
+    import tempfile
+    from gobpfld_amd import kcache
+    if not lib.has("set_kernel_cache"):
+        return 0
+    d = getattr(precompile, "dir", None) or tempfile.mkdtemp(prefix="xe-kernels-")
+    precompile.dir = kcache.enable(lib, d)
+    uniq = kernel_sources(lib, cases)
     kcache.fill(uniq, d)
     return len(uniq)
 

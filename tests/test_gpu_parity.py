@@ -10,7 +10,7 @@ import pytest
 from gobpfld_amd import workloads as W
 from gobpfld_amd.emulator import EmulatorError, ENGINE_INTERP, ENGINE_JIT, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, VM, Settings
 from kats import KATS
-from parity import assert_same, config_case, packets, precompile, run_one
+from parity import assert_same, config_case, packets, run_one
 
 pytestmark = pytest.mark.gpu
 ENGINES = [ENGINE_INTERP, ENGINE_JIT]
@@ -19,32 +19,13 @@ FUZZ_COUNTS = {ENGINE_INTERP: 240, ENGINE_JIT: 48}
 CONFIGS = [("c1", 1024, None), ("c2", 65536, None), ("c3", 30000, 8192), ("c4", 8192, None), ("c5", 30000, 8192)]
 
 
-@pytest.fixture(scope="module", autouse=True)
-def _kernels_built(gpu_lib):
-    """Every per-program kernel this module runs, built up front in parallel (xe_prepare in a thread
-    pool): the KATs, the reduced configs and the fuzz programs on the JIT engine."""
-    from fuzz import gen_program
-    cases = [(k["program"], k["maps"], k["entries"], Settings(engine=ENGINE_JIT)) for k in KATS]
-    for name, n, cap in CONFIGS:
-        prog, maps, entries, _, _ = config_case(name, 16, cap)
-        cases.append((prog, maps, entries, Settings(engine=ENGINE_JIT)))
-    for seed in range(FUZZ_COUNTS[ENGINE_JIT]):
-        prog, maps, entries, settings = gen_program(seed, 24 + seed % 64)
-        settings.engine = ENGINE_JIT
-        cases.append((prog, maps, entries, settings))
-    precompile(gpu_lib, cases)
-
-
 @pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("k", KATS, ids=[k["name"] for k in KATS])
 def test_kat_device_equals_oracle(gpu_lib, oracle_lib, k, engine):
     umem, descs = packets(64, k["pkt"], seed=7)
-    try:
-        a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"], settings=Settings(engine=engine))
-    except EmulatorError as e:
-        # calls, tail calls and ordered maps live in the interpreter's general model only
-        assert engine == ENGINE_JIT and "general model" in str(e), str(e)
-        pytest.skip("interpreter-only program")
+    # every KAT runs on both engines: calls, tail calls, indirect helpers and the ordered maps take the
+    # per-program kernel's dynamic form (xe_jit.cpp generate_dynamic)
+    a = run_one(gpu_lib, k["program"], k["maps"], umem, descs, entries=k["entries"], settings=Settings(engine=engine))
     assert a[0].stats["engine_used"] == engine
     b = run_one(oracle_lib, k["program"], k["maps"], umem, descs, entries=k["entries"])
     assert_same(a, b, k["name"])
@@ -159,3 +140,20 @@ def test_fuzz_device_equals_oracle(gpu_lib, oracle_lib, engine, count):
         a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, settings=settings)
         assert a[0].stats["engine_used"] == engine
         assert_same(a, b, f"fuzz seed {seed}")
+
+
+@pytest.mark.parametrize("engine", ENGINES, ids=ENGINE_IDS)
+def test_bpf2bpf_calls_device_equals_oracle(gpu_lib, oracle_lib, engine):
+    """The call-heavy analogue of cmd/examples/bpf_to_bpf/src/xdp.c (workloads.prog_bpf2bpf: two
+    bpf-to-bpf calls per packet, lifted `stats->pkts++` inside the callee) on both engines: results,
+    verdicts and the three stats maps equal the oracle, and the batch stays parallel (lifted adds in the
+    callee). With register records the loaded values must be exact, so that batch replays in order."""
+    prog, maps, entries, umem, descs = config_case("bpf2bpf", 65536)
+    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, regs=False, settings=Settings(engine=engine))
+    b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=False)
+    assert_same(a, b, "bpf2bpf")
+    assert a[0].stats["engine_used"] == engine and a[0].stats["mode_used"] == MODE_PARALLEL, a[0].stats
+    umem, descs = umem[: 4096 * 64], descs[:4096]
+    a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, regs=True, settings=Settings(engine=engine))
+    b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=True)
+    assert_same(a, b, "bpf2bpf regs")

@@ -17,7 +17,7 @@ from gobpfld_amd import workloads as W
 from gobpfld_amd.asm import JEQ, JGT, Asm, XDP_DROP, XDP_PASS
 from gobpfld_amd.emulator import (MAP_ARRAY, MAP_HASH, MODE_KEYED, MODE_PARALLEL, MODE_SEQUENTIAL, VM, MapDef,
                                   Settings)
-from parity import assert_same, config_case, packets, precompile, run_one
+from parity import assert_same, config_case, packets, run_one
 
 LSH, OR, AND = 0x60, 0x40, 0x50
 
@@ -294,24 +294,10 @@ def test_keyed_batches_hostsim(oracle_lib, hostsim_lib):
 
 
 # ------------------------------------------------------------------ MI355X
-@pytest.fixture(scope="module")
-def _keyed_kernels(gpu_lib):
-    """The per-program kernels (and keyed variants) of this module's device tests, built in parallel."""
-    cases = [(*CASES[c](), Settings(engine=2)) for c in sorted(CASES)]
-    prog, maps, entries, _, _ = config_case("c3learn", 16)
-    cases.append((prog, maps, entries, Settings(engine=2)))
-    cases.append((prog, [(MapDef(MAP_HASH, 16, 16, 2300), None)], config_case("c3learn", 16, flows_cap=2048)[2], Settings()))
-    cases.append((prog_escape(), [(MapDef(MAP_HASH, 4, 8, 64), None), (MapDef(MAP_ARRAY, 4, 8, 8), None)], None,
-                  Settings(engine=2)))
-    cases.append((prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, Settings()))
-    cases.append((prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, Settings()))
-    cases.append((prog_first_seen(), [(MapDef(MAP_HASH, 4, 8, 256), None)], None, Settings()))
-    precompile(gpu_lib, cases)
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("engine", [1, 2], ids=["interp", "jit"])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_keyed_device(gpu_lib, oracle_lib, _keyed_kernels, case, engine):
+def test_keyed_device(gpu_lib, oracle_lib, case, engine):
     prog, maps, entries = CASES[case]()
     umem, descs = packets(100000, 64, seed=23)
     _check(gpu_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_KEYED, case, Settings(engine=engine))
@@ -319,7 +305,7 @@ def test_keyed_device(gpu_lib, oracle_lib, _keyed_kernels, case, engine):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("engine", [1, 2], ids=["interp", "jit"])
-def test_keyed_escape_device(gpu_lib, oracle_lib, _keyed_kernels, engine):
+def test_keyed_escape_device(gpu_lib, oracle_lib, engine):
     umem, descs = packets(20000, 64, seed=24)
     maps = [(MapDef(MAP_HASH, 4, 8, 64), None), (MapDef(MAP_ARRAY, 4, 8, 8), None)]
     _check(gpu_lib, oracle_lib, prog_escape(), maps, None, umem, descs, MODE_SEQUENTIAL, "escape", Settings(engine=engine))
@@ -327,20 +313,20 @@ def test_keyed_escape_device(gpu_lib, oracle_lib, _keyed_kernels, engine):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("engine", [1, 2], ids=["interp", "jit"])
-def test_c3learn_device(gpu_lib, oracle_lib, _keyed_kernels, engine):
+def test_c3learn_device(gpu_lib, oracle_lib, engine):
     prog, maps, entries, umem, descs = config_case("c3learn", 1 << 18)
     _check(gpu_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_KEYED, "c3learn", Settings(engine=engine))
 
 
 @pytest.mark.gpu
-def test_c3learn_capacity_device(gpu_lib, oracle_lib, _keyed_kernels):
+def test_c3learn_capacity_device(gpu_lib, oracle_lib):
     prog, _, entries, umem, descs = config_case("c3learn", 20000, flows_cap=2048)
     maps = [(MapDef(MAP_HASH, 16, 16, 2300), None)]
     _check(gpu_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_SEQUENTIAL, "capacity")
 
 
 @pytest.mark.gpu
-def test_keyed_batches_device(gpu_lib, oracle_lib, _keyed_kernels):
+def test_keyed_batches_device(gpu_lib, oracle_lib):
     prog, maps, entries, _, _ = config_case("c3learn", 16)
     batches = [W.build_batch("c3learn", k * 100000, 100000) for k in range(3)]
     a, da = _batches(gpu_lib, prog, maps, entries, batches)
@@ -352,12 +338,12 @@ def test_keyed_batches_device(gpu_lib, oracle_lib, _keyed_kernels):
 
 
 @pytest.mark.gpu
-def test_keyed_tombstones_device(gpu_lib, oracle_lib, _keyed_kernels):
+def test_keyed_tombstones_device(gpu_lib, oracle_lib):
     _tombstones(gpu_lib, oracle_lib, 50000)
 
 
 @pytest.mark.gpu
-def test_keyed_d_table_retry_device(gpu_lib, oracle_lib, _keyed_kernels):
+def test_keyed_d_table_retry_device(gpu_lib, oracle_lib):
     umem, descs = packets(60000, 64, seed=26)
     _check(gpu_lib, oracle_lib, prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, umem, descs,
            MODE_KEYED, "many_keys")
@@ -365,7 +351,7 @@ def test_keyed_d_table_retry_device(gpu_lib, oracle_lib, _keyed_kernels):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("engine", [1, 0], ids=["interp", "auto"])
-def test_keyed_call_and_packet_write_device(gpu_lib, oracle_lib, _keyed_kernels, engine):
+def test_keyed_call_and_packet_write_device(gpu_lib, oracle_lib, engine):
     umem, descs = packets(50000, 64, seed=30)
     _check(gpu_lib, oracle_lib, prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, umem, descs,
            MODE_KEYED, "call + packet write", Settings(engine=engine))
@@ -374,7 +360,7 @@ def test_keyed_call_and_packet_write_device(gpu_lib, oracle_lib, _keyed_kernels,
 @pytest.mark.gpu
 @pytest.mark.parametrize("engine", [1, 2], ids=["interp", "jit"])
 @pytest.mark.parametrize("case", ["last_len", "two_keys"])
-def test_keyed_register_records_device(gpu_lib, oracle_lib, _keyed_kernels, case, engine):
+def test_keyed_register_records_device(gpu_lib, oracle_lib, case, engine):
     prog, maps, entries = CASES[case]()
     umem, descs = packets(40000, 64, seed=31)
     a = run_one(gpu_lib, prog, maps, umem, descs, entries=entries, regs=True, settings=Settings(engine=engine))

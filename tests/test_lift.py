@@ -155,3 +155,22 @@ def test_c2rmw_device_parallel(gpu_lib, oracle_lib, engine):
     b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=False)
     assert_same(a, b, "c2rmw")
     assert a[0].stats["mode_used"] == MODE_PARALLEL and a[0].stats["conflict"] == 0
+
+
+def test_lift_through_bpf_to_bpf_calls(oracle_lib, hostsim_lib):
+    """lift_rmw follows bpf-to-bpf calls (a call flows into its callee and on to the return site): the
+    `stats->pkts++` / `stats->bytes += size` inside workloads.prog_bpf2bpf's callee are lifted, so the
+    batch runs in parallel and still equals the oracle's sequential VM."""
+    prog, maps, entries, umem, descs = config_case("bpf2bpf", 2000)
+    a = run_one(hostsim_lib, prog, maps, umem, descs, entries=entries, regs=False)
+    b = run_one(oracle_lib, prog, maps, umem, descs, entries=entries, regs=False)
+    assert_same(a, b, "bpf2bpf")
+    assert a[0].stats["mode_used"] == 1, a[0].stats
+    from gobpfld_amd import _native as N
+    import ctypes as C
+    lib = C.CDLL(str(N.PRODUCT_LIB))
+    raw = np.ascontiguousarray(np.asarray(prog, dtype=np.uint64))
+    out = np.zeros(len(raw) * 16, dtype=np.uint8)
+    n = lib.xe_translate_uops(raw.ctypes.data_as(C.c_void_p), len(raw), out.ctypes.data_as(C.c_void_p), len(raw))
+    fl = out.reshape(-1, 16)[:n, 3]
+    assert int(((fl & 0x40) != 0).sum()) == 4     # two load/store pairs in the callee

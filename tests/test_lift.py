@@ -101,13 +101,22 @@ def test_lift_static_pattern():
         return _lifted(a.assemble())
     assert jump_into_middle() == []
 
-    def with_call():
+    def with_call(callee_reads_r1: bool, caller_reads_r1: bool = False):
         a = Asm()
         a.ld_map_value(6, 1).ldx(8, 1, 6, 0).add64(1, 1).stx(8, 6, 0, 1)
-        a.call_bpf("f").mov64(0, 2).exit()
-        a.label("f").mov64(0, 0).exit()
+        a.call_bpf("f")
+        if caller_reads_r1:
+            a.mov64(0, src=1).exit()
+        else:
+            a.mov64(0, 2).exit()
+        a.label("f")
+        a.mov64(0, src=1) if callee_reads_r1 else a.mov64(0, 0)
+        a.exit()
         return _lifted(a.assemble())
-    assert with_call() == []
+    # liveness follows the call into the callee and, past its exit, to the return site
+    assert with_call(False) == [2, 4]
+    assert with_call(True) == []           # R1 is the callee's argument
+    assert with_call(False, True) == []    # R1 survives the return (R0..R5 are not restored)
 
 
 def _maps():

@@ -1243,7 +1243,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
-  dev_free(vm->d_usnap);
+  dev_free(vm->d_usnap); dev_free(vm->d_ovl);
   keyed_free(vm);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
 #ifndef XE_HOSTSIM

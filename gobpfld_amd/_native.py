@@ -89,6 +89,7 @@ _SIGS = {
     "set_kernel_cache": (C.c_int, [C.c_char_p]),
     "kernel_source": (C.c_int, [P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "compile_kernel_source": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "kernel_object_name": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
     "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
@@ -125,7 +126,7 @@ HEADER_SYMBOLS = [
     "xe_device_count", "xe_shard_check", "xe_epoch_begin", "xe_epoch_end", "xe_map_state_bytes", "xe_map_state_export",
     "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error", "xe_debug_set_schedule",
-    "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source",
+    "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source", "xe_kernel_object_name",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h
 
@@ -165,4 +166,8 @@ def product() -> Lib:
         except ImportError:
             pass
         _product = Lib(os.environ.get("XE_LIB", PRODUCT_LIB), "xe_")
+        # the package's ahead-of-time kernel cache (gobpfld_amd/aot.py), when it was built
+        kdir = ROOT / "gobpfld_amd" / "kernels"
+        if kdir.is_dir() and _product.has("set_kernel_cache"):
+            _product.set_kernel_cache(str(kdir).encode())
     return _product

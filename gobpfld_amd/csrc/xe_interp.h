@@ -241,16 +241,29 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #define XE_CM_ALL 127u
 
 // Packet header window staged in LDS per lane (the first 64 bytes are the hot bytes).
-// The window is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR destination) from the 16-byte
-// aligned address below the packet start, as XE_HDR_ROWS rows of 16 bytes per lane; one DMA
-// instruction writes one row for the whole wave, lane-linear (row k of lane l at k * XE_HDR_ROW +
-// l * 16). A lane's logical byte b lives at physical byte b + hsh (hsh = addr & 15) of its rows.
+// The window covers the packet bytes [XE_HDR_LO, XE_HDR_HI) a program can read: the per-program
+// generator derives them from a packet-offset interval analysis (xe_jit.cpp packet_read_range), the
+// shared interpreter keeps [0, 64). It is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR
+// destination) from the 16-byte aligned address at or below packet byte XE_HDR_LO, as up to
+// XE_HDR_ROWS rows of 16 bytes per lane — only the rows that hold bytes of [XE_HDR_LO, min(len,
+// XE_HDR_HI)), so a program that reads 30 header bytes moves one or two 64-B blocks, not always two;
+// one DMA instruction writes one row for the whole wave, lane-linear (row k of lane l at
+// k * XE_HDR_ROW + l * 16). A lane's logical byte b lives at physical byte b + hsh of its rows
+// (hsh = ((addr + XE_HDR_LO) & 15) - XE_HDR_LO). Reads outside the window go to HBM, so the window
+// bounds only decide speed, never results.
 // Two such buffers per wave: the next chunk's window is in flight while the current one executes.
-#define XE_HDR_WIN 64
-#define XE_HDR_ROWS 4                              // 64 bytes from the aligned-down packet address
+#ifndef XE_HDR_LO
+#define XE_HDR_LO 0
+#endif
+#ifndef XE_HDR_HI
+#define XE_HDR_HI 64
+#endif
+#define XE_HDR_SPAN_ROWS ((XE_HDR_HI - XE_HDR_LO + 30) / 16)  // rows for the span at any 16-B phase
+#define XE_HDR_ROWS (XE_HDR_HI <= XE_HDR_LO ? 0 : XE_HDR_SPAN_ROWS < 4 ? XE_HDR_SPAN_ROWS : 4)
 #define XE_HDR_ROW (XE_WAVE * 16)                  // bytes of one row for the whole wave
 #define XE_HDR_BUF (XE_HDR_ROWS * XE_HDR_ROW)      // one buffer
 #define XE_HDR_WAVE_BYTES (2 * XE_HDR_BUF)         // double buffer per wave
+#define XE_HDR_LDS_BYTES (4 * XE_HDR_WAVE_BYTES > 16 ? 4 * XE_HDR_WAVE_BYTES : 16)  // per 256-thread block
 
 // kernel-internal error encoding
 #define XE_EV_PANIC 0x1000
@@ -362,8 +375,8 @@ struct XeLane {
   XE_LP(uint8_t) hdr;      // this lane's column of the current LDS header buffer (+ lane * 16)
   XE_LP(uint8_t) hdrbuf;   // the wave's two header buffers (wave-uniform)
   XE_LP(const XeDevMap) maps;  // map descriptor table (LDS copy of P.maps, stage_maps)
-  int32_t hdr_len;         // min(plen, 64): bytes served from the window
-  int32_t hsh;             // physical offset of logical byte 0 in the lane's rows
+  int32_t hdr_len;         // logical bytes [XE_HDR_LO, hdr_len) are served from the window
+  int32_t hsh;             // physical offset of logical byte 0 in the lane's rows (may be negative)
   // per-lane map footprints for maps 1..4 (others go straight to global)
   uint64_t fpr[XE_FP_MAPS];
   uint64_t fpa[XE_FP_MAPS];
@@ -1070,15 +1083,21 @@ XE_DEV void hdr_write(XeLane& L, int off, int size, uint64_t x) {
 }
 
 // packet ByteMemory access through the header window when possible
+XE_DEV bool in_window(const XeLane& L, int64_t off, int size) {
+#if XE_HDR_LO > 0
+  if (off < XE_HDR_LO) return false;
+#endif
+  return off + size <= L.hdr_len;
+}
 XE_DEV uint64_t pkt_load(const XeLane& L, int64_t off, int size) {
-  if (off + size <= L.hdr_len) return hdr_read(L, int(off), size);
+  if (in_window(L, off, size)) return hdr_read(L, int(off), size);
   uint64_t x = load_le(L.pkt + off, size);
   xe_pin(x);  // wait here, on the rare path, not at the join (where it would drain the prefetch)
   return x;
 }
 XE_DEV void pkt_store(XeLane& L, int64_t off, int size, uint64_t x) {
   store_le(L.pkt + off, size, x);
-  if (off + size <= L.hdr_len) hdr_write(L, int(off), size, x);
+  if (in_window(L, off, size)) hdr_write(L, int(off), size, x);
 }
 
 // Atomic little-endian add of `add` into the `size`-byte field at p (any alignment), truncating
@@ -2570,27 +2589,45 @@ XE_DEV void glds16(XE_GP(const uint8_t) src, uint32_t d) {
 }
 #endif
 
-// Issue the LDS-DMA of a packet's header window into buffer `buf` (wave-uniform). Returns false
-// (nothing issued for this lane) when the rows would run past the UMEM; lane_stage then copies the
-// bytes one by one. The rows start at the 16-byte aligned address below the packet, so a misaligned
-// packet's window holds 64 - (addr & 15) of its bytes (lane_stage sets hdr_len accordingly).
-XE_DEV bool hdr_issue(const XeParams& P, XE_LP(uint8_t) buf, uint64_t a, bool valid) {
-  const uint64_t al = a & ~uint64_t(15);
-  const bool fast = valid && al + XE_HDR_WIN <= P.umem_len;
+// Rows of a packet's header window: those holding bytes of [XE_HDR_LO, min(len, XE_HDR_HI)) counted
+// from the 16-byte aligned address at or below byte XE_HDR_LO (0 when the packet ends before it).
+XE_DEV int hdr_rows(uint64_t a, uint32_t l) {
+#if XE_HDR_ROWS == 0
+  (void)a; (void)l;
+  return 0;
+#else
+  const int end = l < uint32_t(XE_HDR_HI) ? int(l) : XE_HDR_HI;
+  if (end <= XE_HDR_LO) return 0;
+  const int r = (end - XE_HDR_LO + int((a + XE_HDR_LO) & 15) + 15) >> 4;
+  return r < XE_HDR_ROWS ? r : XE_HDR_ROWS;
+#endif
+}
+
+// Issue the LDS-DMA of a packet's header window into buffer `buf` (wave-uniform): row k on the lanes
+// whose window has more than k rows. Returns false (nothing issued for this lane) when the rows would
+// run past the UMEM; lane_stage then copies the bytes one by one.
+XE_DEV bool hdr_issue(const XeParams& P, XE_LP(uint8_t) buf, uint64_t a, uint32_t l, bool valid) {
+#if XE_HDR_ROWS == 0
+  (void)P; (void)buf; (void)a; (void)l; (void)valid;
+  return false;
+#else
+  const uint64_t al = (a + XE_HDR_LO) & ~uint64_t(15);
+  const int nr = valid ? hdr_rows(a, l) : 0;
+  const bool fast = valid && al + 16 * uint64_t(nr) <= P.umem_len;
   if (fast) {
 #if defined(__HIPCC__)
     XE_GP(const uint8_t) src = (XE_GP(const uint8_t))(P.umem + al);
     const uint32_t d = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(buf)))));
-    glds16(src, d);
-    glds16(src + 16, d + XE_HDR_ROW);
-    glds16(src + 32, d + 2 * XE_HDR_ROW);
-    glds16(src + 48, d + 3 * XE_HDR_ROW);
-#else
+#pragma unroll
     for (int k = 0; k < XE_HDR_ROWS; k++)
+      if (k < nr) glds16(src + 16 * k, d + k * XE_HDR_ROW);
+#else
+    for (int k = 0; k < nr; k++)
       for (int b = 0; b < 16; b++) buf[k * XE_HDR_ROW + b] = P.umem[al + 16 * k + b];
 #endif
   }
   return fast;
+#endif
 }
 
 // the LDS-DMA writes of this wave have landed (the compiler does not track them for LDS reads)
@@ -2627,16 +2664,18 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   L.plen = 0;
   L.hdr_len = 0;
   L.hdr = buf + (col < 0 ? xe_lane() : col) * 16;  // col: the staged packet's column (sequential mode)
-  L.hsh = fast ? int(a & 15) : 0;
+  const int sh = fast ? int((a + XE_HDR_LO) & 15) : 0;
+  L.hsh = sh - XE_HDR_LO;
   if (valid) {
     L.pkt = P.umem + a;
     L.plen = int64_t(l);
-    const int win = XE_HDR_WIN - L.hsh;
-    const int hl = l < uint32_t(win) ? int(l) : win;
+    const int nr = hdr_rows(a, l);
+    const int win = XE_HDR_LO + 16 * nr - sh;  // end of the window's logical bytes
+    const int hl = nr == 0 ? 0 : l < uint32_t(win) ? int(l) : win;
     L.hdr_len = hl;
     if (!fast) {
 #pragma unroll 1
-      for (int b = 0; b < hl; b++) *hdr_at(L, b) = ((XE_GP(const uint8_t))L.pkt)[b];
+      for (int b = XE_HDR_LO; b < hl; b++) *hdr_at(L, b + L.hsh) = ((XE_GP(const uint8_t))L.pkt)[b];
     }
   }
   L.ingress = P.ingress;
@@ -2648,7 +2687,7 @@ XE_DEV void lane_reset(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   uint64_t a;
   uint32_t l;
   desc_fetch(P, i, valid, a, l);
-  const bool fast = hdr_issue(P, L.hdrbuf, a, valid);
+  const bool fast = hdr_issue(P, L.hdrbuf, a, l, valid);
   hdr_wait();
   lane_stage(L, P, valid, a, l, fast, L.hdrbuf);
 }
@@ -2672,7 +2711,7 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
     if (P.seq_prefetch) {
       const bool v = lane < m;
       desc_fetch(P, c0 + lane, v, a, l);
-      f = hdr_issue(P, L.hdrbuf, a, v);
+      f = hdr_issue(P, L.hdrbuf, a, l, v);
       hdr_wait();
     }
 #pragma unroll 1
@@ -2740,7 +2779,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
   uint64_t r1lo, r1hi;  // raw descriptor of chunk c1, in flight
   desc_load(P, i1, v1, r1lo, r1hi);
   uint32_t cur = 0;  // buffer of chunk c (wave-uniform)
-  bool f0 = hdr_issue(P, L.hdrbuf, a0, v0);
+  bool f0 = hdr_issue(P, L.hdrbuf, a0, l0, v0);
   L.defer = XE_DEFER_COMMIT != 0;
   L.dv_i = -1;
   for (;;) {
@@ -2750,7 +2789,7 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     uint64_t a1;
     uint32_t l1;
     desc_fix(P, r1lo, r1hi, a1, l1);
-    const bool f1 = hdr_issue(P, L.hdrbuf + (cur ^ 1u) * XE_HDR_BUF, a1, v1);
+    const bool f1 = hdr_issue(P, L.hdrbuf + (cur ^ 1u) * XE_HDR_BUF, a1, l1, v1);
     const uint32_t c2 = c1 + nwaves;
     const uint32_t i2 = chunk_base(P, c2, nchunks) + lane;
     const bool v2 = c2 < nchunks && pkt_in_pass(P, i2);

@@ -10,7 +10,7 @@
 #include <hipcub/device/device_radix_sort.hpp>
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[4 * XE_HDR_WAVE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[XE_HDR_LDS_BYTES];
   __shared__ XePend pend_lds[4];
   extern __shared__ __attribute__((aligned(16))) uint8_t xe_dyn_lds[];  // (nmaps + 1) map descriptors
   XeLane L;  // general lane model: objects, frames and clones in the P.gen arena

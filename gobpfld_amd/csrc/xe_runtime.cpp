@@ -41,13 +41,15 @@ extern "C" void* xe_jit_get(const XeUop* const* progs, const uint32_t* lens, uin
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
-extern "C" int xe_jit_may_write_entries(const XeUop* prog, size_t n);
-extern "C" size_t xe_jit_source_for(const XeUop* const* progs, const uint32_t* lens, uint32_t nprogs, int32_t entry,
-                                    const XeDevMap* maps, uint32_t nmaps, int keyed, char* buf, size_t buflen);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
 #endif
+
+// the kernel generator (xe_jit.cpp; in the host simulation too: sources only, no compiles)
+extern "C" int xe_jit_may_write_entries(const XeUop* prog, size_t n);
+extern "C" size_t xe_jit_source_for(const XeUop* const* progs, const uint32_t* lens, uint32_t nprogs, int32_t entry,
+                                    const XeDevMap* maps, uint32_t nmaps, int keyed, char* buf, size_t buflen);
 
 #define XE_FRAME_SIZE 256  // DefaultVMSettings().StackFrameSize (emulator/vm.go:291-296)
 
@@ -64,7 +66,7 @@ int dmemset(void* d, int v, size_t n, xe_stream_t) { memset(d, v, n); return 0; 
 int dsync(xe_stream_t) { return 0; }
 int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeLane L;
-  static thread_local uint8_t hdrbuf[XE_HDR_WAVE_BYTES];  // one per host thread (xe_multi runs shards concurrently)
+  static thread_local uint8_t hdrbuf[XE_HDR_WAVE_BYTES + 16];  // one per host thread (xe_multi runs shards concurrently)
   L.hdrbuf = hdrbuf;
   XePend pend;
   stage_maps(L, *P, nullptr);
@@ -1741,13 +1743,8 @@ void* keyed_kernel(xe_vm* vm, void* jit) {
 }
 
 bool keyed_candidate(const xe_vm* vm) {
-#ifndef XE_HOSTSIM
   const auto& prog = vm->programs[vm->entry];
   return vm->settings.mode == XE_MODE_AUTO && xe_jit_may_write_entries(prog.data(), prog.size()) != 0;
-#else
-  (void)vm;
-  return false;
-#endif
 }
 
 // parallel-mode grid for the selected kernel (resident blocks; the general model's arena bounds it)
@@ -2234,10 +2231,8 @@ int xe_prepare(xe_vm* vm) {
 // 1: its keyed variant), for a process that fills the kernel cache (xe_compile_kernel_source).
 int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len) {
   if (!vm || (variant != 0 && variant != 1)) return XE_ERR_INVAL;
-#ifdef XE_HOSTSIM
-  (void)buf; (void)cap; (void)len;
-  return fail(vm, XE_ERR_UNSUPPORTED, "no per-program kernels in the host simulation");
-#else
+  // the host simulation generates the same sources (ahead-of-time kernel builds on a machine without a
+  // GPU: gobpfld_amd/aot.py) but runs none of them
   if (int rc = xe_sync(vm)) return rc;
   if (int rc = prepare_run(vm, vm->stream)) return rc;
   if (vm->settings.engine == XE_ENGINE_INTERP || !jit_possible(vm))
@@ -2248,16 +2243,16 @@ int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len)
                                      vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), variant, buf, cap);
   if (len) *len = n;
   return XE_OK;
-#endif
 }
 
 #ifdef XE_HOSTSIM
-// the host simulation builds no per-program kernels (xe_jit.cpp is not part of it)
+// the host simulation compiles no per-program kernels (it links only the generator of xe_jit.cpp)
 int xe_set_kernel_cache(const char*) { return XE_OK; }
 int xe_compile_kernel_source(const char*, const char*, const char*, char* err, size_t errlen) {
   if (err && errlen) err[0] = 0;
   return XE_ERR_UNSUPPORTED;
 }
+int xe_kernel_object_name(const char*, const char*, char*, size_t) { return XE_ERR_UNSUPPORTED; }
 #endif
 
 int xe_sync(xe_vm* vm) {

@@ -64,6 +64,16 @@ def default_workers() -> int:
     return max(1, min(16, n))
 
 
+def code_object_name(src: str, arch: str = "gfx950", lib_path: str | os.PathLike | None = None) -> str:
+    """File name of the code object `src` compiles to in a cache directory (no device needed)."""
+    from . import _native as N
+    lib = N.Lib(lib_path or os.environ.get("XE_LIB", N.PRODUCT_LIB), "xe_")
+    buf = C.create_string_buffer(128)
+    if lib.kernel_object_name(src.encode(), arch.encode(), buf, len(buf)) != 0:
+        raise RuntimeError("xe_kernel_object_name failed")
+    return buf.value.decode()
+
+
 def fill(sources, cache_dir: str | os.PathLike, arch: str = "gfx950", workers: int | None = None,
          lib_path: str | os.PathLike | None = None) -> list[str]:
     """Compile every distinct source into `cache_dir` with a pool of worker processes; returns the

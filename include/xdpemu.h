@@ -355,6 +355,8 @@ const char* xe_multi_last_error(const xe_multi* m);
 int xe_set_kernel_cache(const char* dir);
 int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len);
 int xe_compile_kernel_source(const char* src, const char* arch, const char* dir, char* err, size_t errlen);
+/* the file name (in the cache directory) of the code object a source compiles to for `arch` */
+int xe_kernel_object_name(const char* src, const char* arch, char* buf, size_t cap);
 
 /* --- debug hooks (no reference counterpart) ---
  * Permute the chunk -> wave schedule of the parallel passes (0 = the default walk; s > 0 = a fixed

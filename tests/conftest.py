@@ -43,28 +43,28 @@ def gpu_lib(built):
 
 @pytest.fixture(scope="session", autouse=True)
 def _kernel_cache(request):
-    """GPU sessions: build every per-program kernel the suite uses in worker processes, in the
-    background, into a session kernel cache (gobpfld_amd/kcache.py; hiprtc compiles one kernel at a time
-    per process). Tests start at once and load their kernels from the cache when it has them; a test
-    that gets there first compiles its own, exactly as without the cache."""
+    """GPU sessions: the per-program kernels the suite uses come from the package's ahead-of-time kernel
+    cache (gobpfld_amd/kernels, filled by build() on a CPU machine: gobpfld_amd/aot.py). Whatever it
+    misses (a source changed since) is built in the background by worker processes while the tests run;
+    a test that gets there first compiles its own kernel, exactly as without a cache."""
     if not any(item.get_closest_marker("gpu") for item in request.session.items):
         yield None
         return
-    import tempfile
     import threading
     import torch
     if not torch.cuda.is_available():
         yield None
         return
     from gobpfld_amd import _native as N
+    from gobpfld_amd import aot, kcache
     from gobpfld_amd import build as B
-    from gobpfld_amd import kcache
-    from kernel_cases import gpu_cases
-    from parity import kernel_sources
     B.build_all()
-    lib = N.product()
-    d = kcache.enable(lib, tempfile.mkdtemp(prefix="xe-kernels-"))
-    sources = kernel_sources(lib, gpu_cases())
-    t = threading.Thread(target=kcache.fill, args=(sources, d), daemon=True)
+    d = kcache.enable(N.product(), aot.KERNEL_DIR)
+
+    def fill():
+        from kernel_cases import gpu_cases
+        kcache.fill(aot.sources(gpu_cases()), d)
+
+    t = threading.Thread(target=fill, daemon=True)
     t.start()
     yield d

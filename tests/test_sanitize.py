@@ -36,7 +36,7 @@ def test_sanitized_oracle_and_hostsim_agree(tmp_path):
     hdrs = sorted(csrc.glob("*.h")) + [ROOT / "include" / "xdpemu.h", ROOT / "include" / "xdpemu_io.h"]
     orc = _build(OUT / "liboracle_san.so", [cxx, *FLAGS, "-fPIC", "-shared", str(ROOT / "oracle" / "oracle.cpp")],
                  [ROOT / "oracle" / "oracle.cpp", ROOT / "oracle" / "oracle.h", *hdrs])
-    sim_src = [csrc / "xe_runtime.cpp", csrc / "xe_io.cpp", csrc / "xe_multi.cpp"]
+    sim_src = [csrc / "xe_runtime.cpp", csrc / "xe_io.cpp", csrc / "xe_multi.cpp", csrc / "xe_jit.cpp"]
     sim = _build(OUT / "libxdpemu_hostsim_san.so",
                  [cxx, *FLAGS, "-fPIC", "-shared", "-DXE_HOSTSIM", *map(str, sim_src), "-pthread"], sim_src + hdrs)
     drv = _build(OUT / "san_driver", [cxx, *FLAGS, str(SAN / "san_driver.cpp"), "-ldl"], [SAN / "san_driver.cpp"])

@@ -138,6 +138,28 @@ struct XeDevMap {
   uint32_t pool_cap;
   uint32_t list_cap;
   uint64_t data_cap;
+  // parallel appends (QUEUE / STACK push, PERF output in parallel mode): per pool element / event, the
+  // order key (packet index << 16 | the packet's append number) of the element appended in this run
+  uint64_t* tag;
+};
+
+// One ordered map's appends of a parallel run put in packet order (xe_append_kernel): the new
+// elements / events [base, base + k) sorted by their tags; QUEUE / STACK get the sorted ids in their
+// list positions cnt0 .. cnt0 + k - 1, PERF gets its event records permuted.
+struct XeAppendArgs {
+  uint64_t* tag;             // XeDevMap::tag
+  uint64_t* keys_in;         // [k] scratch
+  uint64_t* keys_out;
+  uint32_t* ids_in;
+  uint32_t* ids_out;
+  uint64_t* rec;             // PERF: XeDevMap::rec
+  uint64_t* rec_tmp;         // PERF: [2k] scratch
+  uint32_t* link;            // LIST: XeDevMap::link
+  uint64_t base;             // first new element id / event index
+  uint64_t head, cnt0, list_cap;
+  uint32_t k;
+  uint32_t perf;
+  uint32_t stack;
 };
 
 XE_HD uint32_t xe_hash_rwords(uint32_t kwords) {

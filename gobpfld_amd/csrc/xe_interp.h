@@ -367,6 +367,8 @@ struct XeLane {
   uint32_t npres;         // PreservedRegisters depth = R10's frame index
   int32_t pi;             // program index (Registers.PI)
   uint32_t npristine;     // private ByteMemories still reading through to their source
+  uint32_t pidx;          // the packet's index in the batch (order key of its parallel appends)
+  uint32_t oseq;          // appends the packet made so far
 #endif
   uint64_t odef;      // ids 1..6 still holding their ctx default
   // packet
@@ -1995,6 +1997,41 @@ XE_COLD int list_push(XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& 
   return 0;
 }
 
+// The same append in parallel mode: element ids / event slots and event bytes are claimed with atomics
+// (in whatever order lanes get there) and each element is tagged with its packet index and the packet's
+// append number; after the run the runtime sorts the run's elements by tag into their list positions /
+// event records (XeAppendArgs), which is the order the packet-by-packet loop appends them in. Push never
+// fails in the reference (an unbounded Go append), so appends commute up to that order.
+XE_COLD int list_push_par(XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, const XeReg& R, int64_t size,
+                          int64_t& err) {
+  err = 0;
+  if (!XE_ISPTR(R.t)) { err = -14; return 0; }
+  if (L.oseq >= 0xffffu) return XE_EV_ORD;  // the tag's append number is 16 bits
+  const uint64_t tag = (uint64_t(L.pidx) << 16) | L.oseq++;
+  if (M.kind == XE_DM_PERF) {
+    int ve = ptr_read_range(L, P, R, size, [&](int64_t, uint8_t) {});
+    if (XE_IS_PANIC(ve)) return ve;
+    const uint64_t n = ve ? 0 : uint64_t(size);
+    const uint64_t c = xe_atomic_add64((unsigned long long*)map_hdr(M, 0), 1ull);
+    const uint64_t used = xe_atomic_add64((unsigned long long*)map_hdr(M, 1), (n + 7) & ~uint64_t(7));
+    if (c >= M.pool_cap || used + n > M.data_cap) return XE_EV_CAP;
+    if (n) ptr_read_range(L, P, R, size, [&](int64_t i, uint8_t b) { ((XE_GP(uint8_t))M.vals)[used + uint64_t(i)] = b; });
+    ((XE_GP(uint64_t))M.rec)[2 * c] = used;
+    ((XE_GP(uint64_t))M.rec)[2 * c + 1] = n;
+    ((XE_GP(uint64_t))M.tag)[c] = tag;
+    return 0;
+  }
+  const uint64_t id = xe_atomic_add64((unsigned long long*)map_hdr(M, 2), 1ull);
+  const uint64_t cnt = xe_atomic_add64((unsigned long long*)map_hdr(M, 1), 1ull);
+  if (id >= M.pool_cap || cnt >= M.list_cap) return XE_EV_CAP;
+  uint8_t* dst = M.vals + id * M.value_size;
+  int e = read_value_into(L, P, R, size, dst);
+  if (XE_IS_PANIC(e)) return e;
+  ((XE_GP(uint32_t))M.elen)[id] = e ? 0u : uint32_t(size);
+  ((XE_GP(uint64_t))M.tag)[id] = tag;
+  return 0;
+}
+
 // TailCall, helper_functions.go:133-210. Returns XE_EV_JUMP on success (PI switched, PC := -1).
 #define XE_EV_JUMP 0x5000
 XE_COLD int helper_tail_call(XeLane& L, const XeParams& P) {
@@ -2043,8 +2080,11 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       if (M.kind != XE_DM_PERF) return helper_errno_result(L, -14);
       const XeReg R5 = reg_get(L, 5);
       XE_NILCHK(R5);
-      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // events are appended in packet order
       int64_t err;
+      if (P.mode == XE_MODE_PARALLEL) {  // appended in packet order after the run (list_push_par)
+        if (int e = list_push_par(L, P, m, M, reg_get(L, 4), R5.v, err)) return in_helper(e);
+        return helper_errno_result(L, err);
+      }
       if (int e = list_push(L, P, m, M, reg_get(L, 4), R5.v, err)) return in_helper(e);
       return helper_errno_result(L, err);
     }
@@ -2054,8 +2094,11 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       if (!m) return 0;
       const XeDevMap M = map_desc(L, m);
       if (M.kind != XE_DM_LIST && M.kind != XE_DM_PERF) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "push not available"
-      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
       int64_t err;
+      if (P.mode == XE_MODE_PARALLEL) {
+        if (int e = list_push_par(L, P, m, M, reg_get(L, 2), int64_t(M.value_size), err)) return in_helper(e);
+        return helper_errno_result(L, err);
+      }
       if (int e = list_push(L, P, m, M, reg_get(L, 2), int64_t(M.value_size), err)) return in_helper(e);
       return helper_errno_result(L, err);
     }
@@ -2797,6 +2840,10 @@ XE_DEV void parallel_packets(XeLane& L, const XeParams& P, uint32_t wave, uint32
     const uint32_t abort_flags = xe_load_relaxed32(P.flags);
     lane_commit(L, P);  // the previous chunk's verdicts and adds, behind this chunk's prefetch
     key_begin(L, i0);
+#if XE_HAS_ORDERED
+    L.pidx = i0;
+    L.oseq = 0;
+#endif
     body(i0, v0);
     if (c1 >= nchunks) break;
     // a lane elsewhere needed an ordered write: this run will be discarded, stop early

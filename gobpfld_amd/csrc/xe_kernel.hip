@@ -232,6 +232,51 @@ extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_b
              : -1;
 }
 
+// One ordered map's parallel appends put in packet order (XeAppendArgs): step 0 gathers the run's tags
+// with the element ids (PERF: and sets the run's event records aside), a radix sort orders them by tag,
+// step 1 writes the sorted ids into the list positions (QUEUE / STACK) or permutes the event records.
+__global__ void xe_append_kernel(XeAppendArgs A, int step) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= A.k) return;
+  if (step == 0) {
+    A.keys_in[j] = A.tag[A.base + j];
+    A.ids_in[j] = uint32_t(A.base + j);
+    if (A.perf) {
+      A.rec_tmp[2 * j] = A.rec[2 * (A.base + j)];
+      A.rec_tmp[2 * j + 1] = A.rec[2 * (A.base + j) + 1];
+    }
+    return;
+  }
+  const uint32_t id = A.ids_out[j];
+  if (A.perf) {
+    const uint64_t o = uint64_t(id) - A.base;
+    A.rec[2 * (A.base + j)] = A.rec_tmp[2 * o];
+    A.rec[2 * (A.base + j) + 1] = A.rec_tmp[2 * o + 1];
+  } else {
+    A.link[A.stack ? A.cnt0 + j : (A.head + A.cnt0 + j) % A.list_cap] = id;
+  }
+}
+
+extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s) {
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, int(A->k), 0, int(end_bit), s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *bytes = tmp;
+    return 0;
+  }
+  if (*bytes < tmp) return -1;
+  const uint32_t blocks = (A->k + 255) / 256;
+  hipLaunchKernelGGL(xe_append_kernel, dim3(blocks), dim3(256), 0, s, *A, 0);
+  if (hipGetLastError() != hipSuccess) return -1;
+  if (hipcub::DeviceRadixSort::SortPairs(scratch, tmp, A->keys_in, A->keys_out, A->ids_in, A->ids_out, int(A->k), 0,
+                                         int(end_bit), s) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(xe_append_kernel, dim3(blocks), dim3(256), 0, s, *A, 1);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // host-side launchers (called from xe_runtime.cpp)
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
   hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);

@@ -41,6 +41,7 @@ extern "C" void* xe_jit_get(const XeUop* const* progs, const uint32_t* lens, uin
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -194,6 +195,24 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, siz
   for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
   return 0;
 }
+int launch_append(const XeAppendArgs* A, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
+  if (!scratch) { *bytes = 8; return 0; }
+  std::vector<std::pair<uint64_t, uint32_t>> v(A->k);
+  for (uint32_t j = 0; j < A->k; j++) v[j] = {A->tag[A->base + j], uint32_t(A->base + j)};
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<uint64_t> rec;
+  if (A->perf) rec.assign(A->rec + 2 * A->base, A->rec + 2 * (A->base + A->k));
+  for (uint32_t j = 0; j < A->k; j++) {
+    const uint32_t id = v[j].second;
+    if (A->perf) {
+      A->rec[2 * (A->base + j)] = rec[2 * (id - A->base)];
+      A->rec[2 * (A->base + j) + 1] = rec[2 * (id - A->base) + 1];
+    } else {
+      A->link[A->stack ? A->cnt0 + j : (A->head + A->cnt0 + j) % A->list_cap] = id;
+    }
+  }
+  return 0;
+}
 struct Timer {
   std::chrono::steady_clock::time_point t;
   void rec(xe_stream_t) { t = std::chrono::steady_clock::now(); }
@@ -235,6 +254,9 @@ int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t
 }
 int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
   return xe_launch_keyed_sort(K, n, end_bit, scratch, bytes, s);
+}
+int launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
+  return xe_launch_append(A, end_bit, scratch, bytes, s);
 }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
@@ -538,6 +560,8 @@ struct HostMap {
   uint32_t pool_cap = 0, list_cap = 0;  // capacities of the device copy (grown on XE_FLAG_CAPACITY)
   uint64_t data_cap = 0;
   uint64_t n_vals = 0, n_elen = 0, n_link = 0, n_rec = 0;  // allocated elements of the device arrays
+  uint64_t* d_tag = nullptr;  // QUEUE / STACK / PERF: order keys of a parallel run's appends (pool_cap)
+  uint64_t n_tag = 0;
   bool ordered() const { return dkind == XE_DM_LRU || dkind == XE_DM_LIST || dkind == XE_DM_PERF; }
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -723,6 +747,11 @@ struct xe_vm {
   // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
   // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
   uint32_t keyed_backoff = 0;
+  // ordered maps: after a parallel try of a batch had to be replayed in order, the next kKeyedBackoff
+  // batches replay straight away; scratch of the append ordering (XeAppendArgs)
+  uint32_t ord_backoff = 0;
+  void* d_app = nullptr; size_t d_app_cap = 0;
+  void* d_app_sort = nullptr; size_t d_app_sort_cap = 0;
   uint32_t sched = 0;  // chunk -> wave schedule permutation of the parallel passes (xe_debug_set_schedule)
 };
 // ---- keyed ordered execution buffers (XeKeyed), sized for n packets
@@ -848,6 +877,9 @@ void map_free_device(HostMap& m) {
   m.pool_cap = m.list_cap = 0;
   m.data_cap = 0;
   m.n_vals = m.n_elen = m.n_link = m.n_rec = 0;
+  dev_free(m.d_tag);
+  m.d_tag = nullptr;
+  m.n_tag = 0;
 }
 
 // Ordered maps on the device (xe_interp.h, general model; XeDevMap comment): rebuilt from the host
@@ -982,6 +1014,7 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
         h2d(m.d_link, link.data(), link.size() * 4, st))
       return -1;
   }
+  if (m.dkind != XE_DM_LRU && ensure_dev(&m.d_tag, m.n_tag, m.pool_cap)) return -1;
   if (!m.d_hdr && dev_alloc((void**)&m.d_hdr, 8 * 8)) return -1;
   if (h2d(m.d_hdr, hdr.data(), 64, st) || dsync(st)) return -1;
   m.host_dirty = false;
@@ -1137,6 +1170,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     d.pool_cap = m.pool_cap;
     d.list_cap = m.list_cap;
     d.data_cap = m.data_cap;
+    d.tag = m.d_tag;
   }
   if (vm->d_maps_n < dm.size()) {
     dev_free(vm->d_maps);
@@ -1245,7 +1279,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
-  dev_free(vm->d_usnap); dev_free(vm->d_ovl);
+  dev_free(vm->d_usnap); dev_free(vm->d_ovl); dev_free(vm->d_app); dev_free(vm->d_app_sort);
   keyed_free(vm);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
 #ifndef XE_HOSTSIM
@@ -1624,6 +1658,58 @@ static bool has_callbpf(const xe_vm* vm) {
       if (u.cls == U_CALLBPF) return true;
   return false;
 }
+// The ordered maps a parallel run can serve: QUEUE / STACK pushes and PERF outputs (appends, put in
+// packet order after the run); any other operation on them (pops, peeks, lookups, every LRU_HASH
+// operation) raises XE_FLAG_ORDERED and the batch replays in packet order. LRU maps: straight away.
+static bool ordered_parallel_ok(const xe_vm* vm) {
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].dkind == XE_DM_LRU) return false;
+  return true;
+}
+// the ordered maps' header words (counts, next ids, event bytes) at the start of a parallel run
+static int ordered_hdr_read(xe_vm* vm, std::vector<uint64_t>& out, xe_stream_t s) {
+  out.assign(vm->maps.size() * 8, 0);
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].ordered() && d2h(&out[i * 8], vm->maps[i].d_hdr, 64, s)) return -1;
+  return dsync(s);
+}
+static int ordered_hdr_restore(xe_vm* vm, const std::vector<uint64_t>& h, xe_stream_t s) {
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].ordered() && h2d(vm->maps[i].d_hdr, &h[i * 8], 64, s)) return -1;
+  return dsync(s);
+}
+// put the appends of a parallel run (header words `h0` before it) into packet order
+static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t n, xe_stream_t s) {
+  std::vector<uint64_t> h1;
+  if (ordered_hdr_read(vm, h1, s)) return -1;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (!m.ordered() || m.dkind == XE_DM_LRU) continue;
+    const bool perf = m.dkind == XE_DM_PERF;
+    const uint64_t base = perf ? h0[i * 8] : h0[i * 8 + 2];
+    const uint64_t k = (perf ? h1[i * 8] : h1[i * 8 + 2]) - base;
+    if (!k) continue;
+    XeAppendArgs A{};
+    const size_t need = size_t(k) * (8 + 8 + 4 + 4 + (perf ? 16 : 0)) + 256;
+    if (ensure_buf(&vm->d_app, &vm->d_app_cap, need)) return -1;
+    uint8_t* b = (uint8_t*)vm->d_app;
+    A.keys_in = (uint64_t*)b; A.keys_out = A.keys_in + k;
+    A.rec_tmp = perf ? A.keys_out + k : nullptr;
+    A.ids_in = (uint32_t*)(A.keys_out + k + (perf ? 2 * k : 0)); A.ids_out = A.ids_in + k;
+    A.tag = m.d_tag; A.rec = m.d_rec; A.link = m.d_link;
+    A.base = base; A.k = uint32_t(k); A.perf = perf ? 1 : 0; A.stack = m.stack ? 1 : 0;
+    A.head = h0[i * 8]; A.cnt0 = h0[i * 8 + 1]; A.list_cap = m.list_cap;
+    // tags: packet index << 16 | append number
+    uint32_t end_bit = 17;
+    while (end_bit < 64 && (uint64_t(1) << (end_bit - 16)) < uint64_t(n) + 1) end_bit++;
+    size_t sb = 0;
+    if (launch_append(&A, end_bit, nullptr, &sb, s) || ensure_buf(&vm->d_app_sort, &vm->d_app_sort_cap, sb) ||
+        launch_append(&A, end_bit, vm->d_app_sort, &sb, s))
+      return -1;
+  }
+  return dsync(s);
+}
+
 static bool has_ordered_maps(const xe_vm* vm) {
   for (size_t i = 1; i < vm->maps.size(); i++)
     if (vm->maps[i].ordered()) return true;
@@ -2077,9 +2163,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
   float kms = 0;
-  const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && !has_ordered_maps(vm);
-  if (mode == XE_MODE_SEQUENTIAL || (mode == XE_MODE_AUTO && has_ordered_maps(vm)) || overlap) {
-    // ordered maps: every operation on them is order-dependent; replay straight away
+  const bool ordmaps = has_ordered_maps(vm);
+  const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && !ordmaps;
+  // ordered maps: appends run in parallel (put in packet order afterwards); a batch with any other
+  // operation on them replays in order, and so do the next few after such a batch
+  bool ord_seq = mode == XE_MODE_AUTO && ordmaps && (!ordered_parallel_ok(vm) || vm->ord_backoff);
+  if (ord_seq && vm->ord_backoff) vm->ord_backoff--;
+  std::vector<uint64_t> ord_h0;
+  if (mode == XE_MODE_SEQUENTIAL || ord_seq || overlap) {
     used = XE_MODE_SEQUENTIAL;
     if (int rc = sequential(kms)) return rc;
   } else if (keyed_ok && vm->keyed_hint) {
@@ -2100,6 +2191,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     P.mode = XE_MODE_PARALLEL;
     vm->last_grid = parallel_grid(vm, jit, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+    if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
     if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
     vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
     if (fold()) return fail(vm, XE_ERR_DEVICE, "replica fold");
@@ -2111,6 +2203,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the
       // keyed path, everything else (and what the keyed path refuses) the replay in packet order
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      if (ordmaps) {  // the appends of the run are past the restored counts: unreferenced
+        if (ordered_hdr_restore(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "rollback (ordered maps)");
+        vm->ord_backoff = kKeyedBackoff;
+      }
       int r = 1;
       const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY);
       if (try_keyed && vm->keyed_backoff) vm->keyed_backoff--;
@@ -2133,6 +2229,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     } else if (!conflict) {
       vm->keyed_backoff = 0;
     }
+    // the run's results stand: its appends into packet order
+    if (ordmaps && used == XE_MODE_PARALLEL && ordered_finalize(vm, ord_h0, n, s))
+      return fail(vm, XE_ERR_DEVICE, "ordered map appends");
   }
   vm->keyed_hint = used == XE_MODE_KEYED;
   if (used == XE_MODE_KEYED) red[0] |= XE_FLAG_ORDERED;  // order-dependent effects (shard checks replay it)
@@ -2555,6 +2654,8 @@ int xe_footprint(xe_vm* vm, uint64_t* out, uint32_t cap_words, uint32_t* nwords)
   uint64_t f = ep ? XE_FPF_EPOCH : 0;
   if (flags & XE_FLAG_ORDERED) f |= XE_FPF_ORDERED;
   if (ep ? vm->epoch_seq : (vm->last_mode == XE_MODE_SEQUENTIAL || vm->last_mode == XE_MODE_KEYED)) f |= XE_FPF_SEQUENTIAL;
+  // ordered maps (appends included) are never summed across shards: their lists follow packet order
+  if (has_ordered_maps(vm)) f |= XE_FPF_SEQUENTIAL;
   if (flags & XE_FLAG_UNALIGNED) f |= XE_FPF_UNALIGNED;
   out[0] = f;
   for (uint32_t m = 1; m <= nm; m++) {

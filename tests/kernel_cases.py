@@ -9,7 +9,8 @@ JIT = 2
 
 
 def gpu_cases():
-    """(program, maps, entries, settings) in roughly the order the suite reaches them."""
+    """(program, maps, entries, settings) — or a function setting a VM up — in roughly the order the
+    suite reaches them."""
     from fuzz import gen_program
     from kats import KATS
     from parity import config_case
@@ -32,4 +33,13 @@ def gpu_cases():
     cases.append((K.prog_many_keys(), [(MapDef(MAP_ARRAY, 4, 8, 16384), None)], None, Settings()))
     cases.append((K.prog_learn_in_call(), [(MapDef(MAP_HASH, 4, 8, 64), None)], None, Settings()))
     cases.append((K.prog_first_seen(), [(MapDef(MAP_HASH, 4, 8, 256), None)], None, Settings()))
+    # the shard-exchange programs (tests/test_multirank.py, test_gpu_multi.py) and the LRU golden program
+    import test_lru_golden as G
+    import test_multirank as M
+    for name, _, cap, _ in M.CASES:
+        cases.append(lambda vm, name=name, cap=cap: M._setup(vm, name, cap))
+    cases.append(lambda vm: vm.set_entrypoint(vm.add_raw_program(G._program(G._map(vm)))))
+    import test_ordered_par as O
+    for build, mdef, entries, _ in O.CASES.values():
+        cases.append((build(), [mdef], entries, Settings()))
     return cases

@@ -42,21 +42,10 @@ def run_one(lib, program, maps, umem, descs, settings=None, regs=True, entries=N
 
 
 def kernel_sources(lib, cases) -> list[str]:
-    """Sources of the per-program kernels of many cases (program, maps, entries, settings), each case's
-    VM set up as run_one does (xe_kernel_source); cases that run on the interpreter contribute none."""
-    from gobpfld_amd.emulator import EmulatorError
-    sources = []
-    for program, maps, entries, settings in cases:
-        try:
-            vm = setup_one(lib, program, maps, settings, entries)[0]
-        except EmulatorError:
-            continue
-        try:
-            sources += vm.kernel_sources()
-        except EmulatorError:
-            pass
-        vm.close()
-    return list(dict.fromkeys(sources))
+    """Sources of the per-program kernels of many cases (gobpfld_amd/aot.py sources: (program, maps,
+    entries, settings) tuples or VM setup functions); cases that run on the interpreter contribute none."""
+    from gobpfld_amd import aot
+    return aot.sources(cases, lib=lib)
 
 
 def precompile(lib, cases) -> int:

@@ -1,0 +1,111 @@
+"""Ordered maps in parallel: QUEUE / STACK pushes and PERF_EVENT_ARRAY outputs run in parallel lanes and
+are put into packet order afterwards (xe_interp.h list_push_par, xe_runtime.cpp ordered_finalize).
+
+The reference appends in its packet-by-packet loop (emulator/vm.go:110-173): QueueMap/StackMap.Push
+(emulator/maps_queue.go:60-77, maps_stack.go:60-77) and PerfEventArray.Push
+(emulator/maps_perf_event_array.go:101-115) are unbounded Go appends, so a batch of appends commutes up
+to the order of the list — which is packet order, and call order within a packet. Every case runs
+against the oracle's single VM (results, register records, the lists in order) and must report
+mode_used PARALLEL; a batch that also pops replays in order (mode SEQUENTIAL) and still matches."""
+import numpy as np
+import pytest
+
+from gobpfld_amd.asm import JEQ, JGT, JNE, Asm
+from gobpfld_amd.emulator import MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_PARALLEL, MODE_SEQUENTIAL, MapDef
+from parity import assert_same, packets, run_one
+
+
+def _head(a, need):
+    a.ldx(4, 6, 1, 0).ldx(4, 7, 1, 4)
+    a.mov64(2, src=6).add64(2, need)
+    a.jmp(JGT, 2, "out", src=7)
+
+
+def prog_push(pop=False):
+    """push u64 packet[0:8]; when packet[8] is odd also push packet[8:16]; pop: when packet[9] == 0
+    pop one element first (order-dependent)."""
+    a = Asm()
+    _head(a, 16)
+    if pop:
+        a.ldx(1, 4, 6, 9).jmp(JNE, 4, "nopop", imm=0)
+        a.ld_map(1, 1).mov64(2, src=10).add64(2, -24).call(88)
+        a.label("nopop")
+    a.ldx(8, 3, 6, 0).stx(8, 10, -8, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -8).mov64(3, 0).call(87)
+    a.ldx(1, 4, 6, 8).alu64(0x50, 4, 1)          # r4 &= 1 (AND)
+    a.jmp(JEQ, 4, "out", imm=0)
+    a.ldx(8, 3, 6, 8).stx(8, 10, -16, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -16).mov64(3, 0).call(87)
+    a.label("out").mov64(0, 2).exit()
+    return a.assemble()
+
+
+def prog_perf():
+    """output packet[0 : 1 + packet[10] % 16] as an event; when packet[11] % 4 == 0 output packet[16:24]
+    as a second one."""
+    a = Asm()
+    _head(a, 32)
+    a.ldx(1, 5, 6, 10).alu64(0x50, 5, 15).add64(5, 1)
+    a.ld_map(2, 1).mov64(4, src=6).mov64(3, 0).call(25)
+    a.ldx(1, 4, 6, 11).alu64(0x50, 4, 3)
+    a.jmp(JNE, 4, "out", imm=0)
+    a.ld_map(2, 1).mov64(4, src=6).add64(4, 16).mov64(5, 8).mov64(3, 0).call(25)
+    a.label("out").mov64(0, 2).exit()
+    return a.assemble()
+
+
+QUEUE = (MapDef(MAP_QUEUE, 0, 8, 16), None)
+STACK = (MapDef(MAP_STACK, 0, 8, 16), None)
+PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
+PRELOAD = {0: [(None, (0xAB00 + i).to_bytes(8, "little")) for i in range(3)]}  # userspace pushes first
+
+CASES = {
+    "queue": (prog_push, QUEUE, PRELOAD, MODE_PARALLEL),
+    "stack": (prog_push, STACK, PRELOAD, MODE_PARALLEL),
+    "perf": (prog_perf, PERF, None, MODE_PARALLEL),
+    "queue_pop": (lambda: prog_push(pop=True), QUEUE, PRELOAD, MODE_SEQUENTIAL),
+}
+
+
+def _run(lib, name, n, seed=11):
+    build, mdef, entries, _ = CASES[name]
+    umem, descs = packets(n, 64, seed=seed)
+    return run_one(lib, build(), [mdef], umem, descs, entries=entries)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_appends_hostsim_equal_oracle(oracle_lib, hostsim_lib, name):
+    got = _run(hostsim_lib, name, 1024)
+    assert_same(got, _run(oracle_lib, name, 1024), name)
+    assert got[0].stats["mode_used"] == CASES[name][3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_appends_device_equal_oracle(gpu_lib, oracle_lib, name):
+    n = 4096 if name == "queue_pop" else 262144
+    got = _run(gpu_lib, name, n)
+    assert_same(got, _run(oracle_lib, name, n), name)
+    assert got[0].stats["mode_used"] == CASES[name][3]
+
+
+@pytest.mark.gpu
+def test_perf_appends_device_two_batches(gpu_lib, oracle_lib):
+    """Two batches into one VM: the second batch's events follow the first's (the parallel order keys
+    restart per batch; the list keeps growing past the device room it started with)."""
+    from gobpfld_amd.emulator import VM, Settings
+    outs = []
+    for lib in (gpu_lib, oracle_lib):
+        vm = VM(Settings(), lib=lib)
+        m = vm.add_map(PERF[0])
+        vm.set_entrypoint(vm.add_raw_program(prog_perf()))
+        modes = []
+        for seed in (3, 4):
+            umem, descs = packets(131072, 64, seed=seed)
+            r = vm.run_batch(umem, descs)
+            modes.append(r.stats["mode_used"])
+        outs.append((vm.map_dump(m), modes))
+        vm.close()
+    (gd, gm), (od, _) = outs
+    assert gm == [MODE_PARALLEL, MODE_PARALLEL]
+    assert len(gd) == len(od) and gd == od

@@ -279,17 +279,23 @@ def single_process_multi(args, name: str, n: int) -> None:
     value = n * G * args.steps / elapsed / 1e6
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = float(alg_bytes_per_packet(name, sizes).sum()) / avg_kernel_s / 1e9
+    traffic, traffic_src = pmc_traffic(name, n)
+    cpu = None if args.no_cpu_baseline else cpu_baseline(name, args.cpu_sample)
     print(json.dumps({
         "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches", "value": round(value, 3),
         "unit": "Mpkt/s", "n_gpus": G, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic splitmix64 packets, SURVEY §8d)",
         "config": {"workload": WORKLOADS[name], "packets_per_gpu": n, "parallelism": f"dp{G} (one process, xe_run_batch_multi)",
-                   "insns_per_packet": round(steps_retired / max(1, n * args.steps), 2), "in_order_replays": replays},
+                   "insns_per_packet": round(steps_retired / max(1, n * args.steps), 2), "in_order_replays": replays,
+                   "batches": "synchronous xe_run_batch_multi: every step runs the shards and reconciles the maps "
+                              "(RCCL delta all-reduce or in-order replay) — an exchange per step, unlike the "
+                              "torchrun form's one exchange per epoch of pipelined batches"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None if traffic is None else int(traffic),
+                     "traffic_source": traffic_src, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "kernel": "device 0 emulator kernel"},
-        "cpu_baseline": None}), flush=True)
+        "cpu_baseline": cpu}), flush=True)
     mu.close()
     for v in vms:
         v.close()

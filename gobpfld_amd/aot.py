@@ -33,9 +33,9 @@ def host_lib() -> N.Lib:
     return N.Lib(HOST_LIB, "xe_")
 
 
-def sources(cases, lib: N.Lib | None = None) -> list[str]:
-    """Kernel sources of VMs set up from `cases`: callables taking a VM (setup functions) or
-    (program, maps, entries, settings) tuples as the test suite lists them."""
+def sources(cases, lib: N.Lib | None = None, variants=(0, 1, 2)) -> list[str]:
+    """Kernel sources (xe_kernel_source `variants`) of VMs set up from `cases`: callables taking a VM
+    (setup functions) or (program, maps, entries, settings) tuples as the test suite lists them."""
     from .emulator import VM, EmulatorError, Settings
     lib = lib or host_lib()
     out = []
@@ -61,7 +61,7 @@ def sources(cases, lib: N.Lib | None = None) -> list[str]:
         except EmulatorError:
             continue
         try:
-            out += vm.kernel_sources()
+            out += vm.kernel_sources(variants)
         except EmulatorError:
             pass
         vm.close()
@@ -74,22 +74,24 @@ def bench_cases() -> list:
     return [(lambda vm, n=name: W.setup_vm(vm, n)) for name in ("c1", "c2", "c2rmw", "c3", "c3learn", "c4", "c5", "bpf2bpf")]
 
 
-def test_cases() -> list:
-    """The -m gpu suite's kernels (tests/kernel_cases.py)."""
+def test_sources() -> list[str]:
+    """The -m gpu suite's kernels (tests/kernel_cases.py): every case's kernel and keyed variant, the
+    verdict-only variant of the cases run without records."""
     tests = str(ROOT / "tests")
     if tests not in sys.path:
         sys.path.insert(0, tests)
-    from kernel_cases import gpu_cases
-    return gpu_cases()
+    from kernel_cases import gpu_cases, gpu_lean_cases
+    return sources(gpu_cases(), variants=(0, 1)) + sources(gpu_lean_cases(), variants=(2,))
 
 
-def build(cases, cache_dir: str | os.PathLike = KERNEL_DIR, workers: int | None = None, prune: bool = False) -> dict:
-    """Compile the kernels of `cases` that the cache does not hold yet. prune: remove the code objects
-    no case needs any more (the directory then holds exactly this set)."""
+def build(srcs: list[str], cache_dir: str | os.PathLike = KERNEL_DIR, workers: int | None = None,
+          prune: bool = False) -> dict:
+    """Compile the kernel sources `srcs` the cache does not hold yet. prune: remove the code objects
+    no source needs any more (the directory then holds exactly this set)."""
     from . import kcache
     d = Path(cache_dir)
     d.mkdir(parents=True, exist_ok=True)
-    srcs = sources(cases)
+    srcs = list(dict.fromkeys(srcs))
     errors = kcache.fill(srcs, d, workers=workers)
     removed = 0
     if prune:
@@ -103,7 +105,7 @@ def build(cases, cache_dir: str | os.PathLike = KERNEL_DIR, workers: int | None 
 
 def build_all(workers: int | None = None, tests: bool = True) -> dict:
     """The benchmark / smoke kernels, and with `tests` the -m gpu suite's (then stale objects are pruned)."""
-    return build(bench_cases() + (test_cases() if tests else []), KERNEL_DIR, workers=workers, prune=tests)
+    return build(sources(bench_cases()) + (test_sources() if tests else []), KERNEL_DIR, workers=workers, prune=tests)
 
 
 if __name__ == "__main__":

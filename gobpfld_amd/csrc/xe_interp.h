@@ -162,6 +162,11 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
   }
 }
 
+// per-packet result / register records (xe_result, xe_regs); 0: a verdict-only kernel variant
+#ifndef XE_RECORDS
+#define XE_RECORDS 1
+#endif
+
 #if defined(XE_MEM_FIELDS)
 #define XE_GEN 0
 #else
@@ -3084,7 +3089,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 #endif
   if (valid) {
     const XeReg R0 = reg_get(L, 0);
-    if (P.results) {
+    if (XE_RECORDS && P.results) {
       xe_result r;
       r.status = uint8_t(status);
       r.r0_kind = uint8_t(XE_T_KIND(R0.t));
@@ -3097,7 +3102,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
       if (L.defer) { L.dv_i = int32_t(i); L.dv = uint32_t(uint64_t(R0.v)); }
       else P.verdicts[i] = uint32_t(uint64_t(R0.v));
     }
-    if (P.regs) {
+    if (XE_RECORDS && P.regs) {
       xe_regs g;
 #pragma unroll
       for (int r = 0; r < 10; r++) {

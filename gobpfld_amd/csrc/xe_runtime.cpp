@@ -696,6 +696,8 @@ struct xe_vm {
   std::string jit_error;
   // its keyed variant (keyed ordered execution), built with it when the program may write map entries
   void* kjit_fn = nullptr;
+  void* ljit_fn = nullptr;   // the verdict-only variant (no result / register records)
+  bool ljit_ready = false;
   bool kjit_ready = false;
   Timer t0, t1, t2;
   // room the ordered maps' device copies keep for one run (elements / events, event bytes), grown
@@ -1795,6 +1797,8 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
       vm->jit_nprogs = vm->programs.size();
       vm->kjit_ready = false;
       vm->kjit_fn = nullptr;
+      vm->ljit_ready = false;
+      vm->ljit_fn = nullptr;
     }
     jit = vm->jit_fn;
     jit_general = vm->jit_general;
@@ -1825,6 +1829,26 @@ void* keyed_kernel(xe_vm* vm, void* jit) {
 #else
   (void)vm; (void)jit;
   return nullptr;
+#endif
+}
+
+// The verdict-only variant of the selected per-program kernel (xe_jit.cpp XE_JV_LEAN) for parallel runs
+// that ask for no result / register records; the plain kernel when it cannot be built.
+void* lean_kernel(xe_vm* vm, void* jit) {
+#ifndef XE_HOSTSIM
+  if (!jit) return nullptr;
+  if (!vm->ljit_ready) {
+    const ProgTab t = prog_tab(vm);
+    bool cy = false, ge = false;
+    const char* jerr = "";
+    vm->ljit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
+                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 2);
+    vm->ljit_ready = true;
+  }
+  return vm->ljit_fn ? vm->ljit_fn : jit;
+#else
+  (void)vm;
+  return jit;
 #endif
 }
 
@@ -2189,10 +2213,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     kms += Timer::ms(vm->t0, vm->t1);
   } else {
     P.mode = XE_MODE_PARALLEL;
-    vm->last_grid = parallel_grid(vm, jit, general, n, P.nmaps);
+    void* pj = (jit && !P.results && !P.regs) ? lean_kernel(vm, jit) : jit;  // verdicts only: the lean variant
+    vm->last_grid = parallel_grid(vm, pj, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
-    if (launch(&P, vm->last_grid, 256)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+    if (pj ? launch_jit(pj, &P, vm->last_grid, 256, s) : launch_interp(&P, vm->last_grid, 256, s))
+      return fail(vm, XE_ERR_DEVICE, "kernel launch");
     vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
     if (fold()) return fail(vm, XE_ERR_DEVICE, "replica fold");
     if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
@@ -2323,13 +2349,15 @@ int xe_prepare(xe_vm* vm) {
   bool jit_general = false;
   if (int rc = select_engine(vm, jit, jit_general)) return rc;
   if (jit && keyed_candidate(vm)) keyed_kernel(vm, jit);
+  if (jit) lean_kernel(vm, jit);
   return dsync(vm->stream) ? fail(vm, XE_ERR_DEVICE, "sync") : XE_OK;
 }
 
-// The generated source of the kernel xe_prepare would build (variant 0: the per-program kernel,
-// 1: its keyed variant), for a process that fills the kernel cache (xe_compile_kernel_source).
+// The generated source of a kernel xe_prepare would build (variant 0: the per-program kernel, 1: its
+// keyed variant, 2: its verdict-only variant), for a process that fills the kernel cache
+// (xe_compile_kernel_source).
 int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len) {
-  if (!vm || (variant != 0 && variant != 1)) return XE_ERR_INVAL;
+  if (!vm || variant < 0 || variant > 2) return XE_ERR_INVAL;
   // the host simulation generates the same sources (ahead-of-time kernel builds on a machine without a
   // GPU: gobpfld_amd/aot.py) but runs none of them
   if (int rc = xe_sync(vm)) return rc;
@@ -2448,6 +2476,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
       words.push_back(m.vals_alloc / 8);
     }
   }
+  if (jit && !P.results && !P.regs) jit = lean_kernel(vm, jit);  // verdicts only: the lean variant
   const uint32_t grid = parallel_grid(vm, jit, general, n, P.nmaps);
   if (general && ensure_arena(vm, false, grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
   if (!src.empty() && launch_prologue(src.data(), dst.data(), words.data(), uint32_t(src.size()), nullptr, 0, s))

@@ -298,11 +298,12 @@ class VM:
         if self.lib.has("prepare"):
             self._check(self.lib.prepare(self.h), "prepare")
 
-    def kernel_sources(self) -> list[str]:
-        """Sources of the per-program kernels xe_prepare would build (the kernel, and its keyed variant
-        when the program may write map entries); [] when the VM runs the interpreter."""
+    def kernel_sources(self, variants=(0, 1, 2)) -> list[str]:
+        """Sources of the per-program kernels xe_prepare would build (0: the kernel, 1: its keyed variant
+        when the program may write map entries, 2: its verdict-only variant); [] when the VM runs the
+        interpreter."""
         out = []
-        for variant in (0, 1):
+        for variant in variants:
             n = C.c_size_t()
             rc = self.lib.kernel_source(self.h, variant, None, 0, C.byref(n))
             if rc == -95:  # XE_ERR_UNSUPPORTED

@@ -350,7 +350,8 @@ const char* xe_multi_last_error(const xe_multi* m);
  * generated source, the interpreter headers, the options and the gfx target); NULL/"" disables it.
  * hiprtc compiles one kernel at a time per process, so a caller with many programs can have other
  * processes fill the cache: xe_kernel_source gives the source xe_prepare would compile (variant 0: the
- * per-program kernel, 1: its keyed-execution variant; XE_ERR_UNSUPPORTED when the VM runs none) and
+ * per-program kernel, 1: its keyed-execution variant, 2: its verdict-only variant — the one parallel
+ * runs without result / register records use; XE_ERR_UNSUPPORTED when the VM runs none) and
  * xe_compile_kernel_source compiles one into the directory without a device. NULL buf queries *len. */
 int xe_set_kernel_cache(const char* dir);
 int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len);

@@ -62,8 +62,7 @@ def _kernel_cache(request):
     d = kcache.enable(N.product(), aot.KERNEL_DIR)
 
     def fill():
-        from kernel_cases import gpu_cases
-        kcache.fill(aot.sources(gpu_cases()), d)
+        kcache.fill(aot.test_sources(), d)
 
     t = threading.Thread(target=fill, daemon=True)
     t.start()

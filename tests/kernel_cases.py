@@ -43,3 +43,20 @@ def gpu_cases():
     for build, mdef, entries, _ in O.CASES.values():
         cases.append((build(), [mdef], entries, Settings()))
     return cases
+
+
+def gpu_lean_cases():
+    """The cases the suite also runs without result records (device-resident batches with verdicts only):
+    their verdict-only kernel variant. The full-size config tests share bench.py's geometry (its kernels
+    come with the benchmark's)."""
+    from parity import config_case
+    cases = []
+    for name, cap in (("c2", None), ("c5", 8192)):
+        prog, maps, entries, _, _ = config_case(name, 16, cap)
+        cases.append((prog, maps, entries, Settings()))
+    import test_lru_golden as G
+    import test_multirank as M
+    for name, _, cap, _ in M.CASES:
+        cases.append(lambda vm, name=name, cap=cap: M._setup(vm, name, cap))
+    cases.append(lambda vm: vm.set_entrypoint(vm.add_raw_program(G._program(G._map(vm)))))
+    return cases

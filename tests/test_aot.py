@@ -53,3 +53,4 @@ def test_host_generated_sources_equal_device_sources(gpu_lib, hostsim_lib, name)
     from gobpfld_amd import aot
     case = _case(name)
     assert aot.sources([case], lib=hostsim_lib) == aot.sources([case], lib=gpu_lib)
+    assert len(aot.sources([case], lib=hostsim_lib, variants=(2,))) == 1  # the verdict-only variant

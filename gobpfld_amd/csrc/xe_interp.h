@@ -66,6 +66,9 @@ XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) {
 XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) {
   __hip_atomic_fetch_or((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+XE_DEV void xe_atomic_max64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_fetch_max((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) {
   return __hip_atomic_fetch_add((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -104,6 +107,10 @@ XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long l
 XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { __atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); return c; }
 XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
 XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
+XE_DEV void xe_atomic_max64(unsigned long long* p, unsigned long long v) {
+  unsigned long long c = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (c < v && !__atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+}
 XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
@@ -1782,9 +1789,17 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
 #endif
 #if XE_HAS_ORDERED
     if (M.kind == XE_DM_LRU) {
-      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // a lookup promotes: a write to the UsageList
       const uint32_t v = lru_find(M, kw, empty);
       if (v == XE_NONE) return 0;
+      if (P.mode == XE_MODE_PARALLEL) {
+        // a lookup promotes (maps_hash_lru.go:70-91): in packet order the key ends up at the head as
+        // often as it was touched last; the run keeps each value's last touch (packet << 16 | call) + 1
+        // and the runtime moves the touched keys to the UsageList's head by it (ordered_finalize)
+        if (L.oseq >= 0xffffu) return XE_EV_ORD;
+        xe_atomic_max64((unsigned long long*)M.tag + v, ((uint64_t(L.pidx) << 16) | L.oseq++) + 1);
+        out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
+        return 0;
+      }
       lru_promote(M, v);
       out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
       return 0;

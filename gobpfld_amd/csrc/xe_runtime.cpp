@@ -561,7 +561,9 @@ struct HostMap {
   uint64_t data_cap = 0;
   uint64_t n_vals = 0, n_elen = 0, n_link = 0, n_rec = 0;  // allocated elements of the device arrays
   uint64_t* d_tag = nullptr;  // QUEUE / STACK / PERF: order keys of a parallel run's appends (pool_cap)
-  uint64_t n_tag = 0;
+  uint64_t n_tag = 0;         // LRU: each value's last touch in a parallel run
+  uint8_t* d_vsnap = nullptr; // LRU: the value pool at a parallel run's start (its adds are rolled back)
+  uint64_t n_vsnap = 0;
   bool ordered() const { return dkind == XE_DM_LRU || dkind == XE_DM_LIST || dkind == XE_DM_PERF; }
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -882,6 +884,9 @@ void map_free_device(HostMap& m) {
   dev_free(m.d_tag);
   m.d_tag = nullptr;
   m.n_tag = 0;
+  dev_free(m.d_vsnap);
+  m.d_vsnap = nullptr;
+  m.n_vsnap = 0;
 }
 
 // Ordered maps on the device (xe_interp.h, general model; XeDevMap comment): rebuilt from the host
@@ -1016,7 +1021,8 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
         h2d(m.d_link, link.data(), link.size() * 4, st))
       return -1;
   }
-  if (m.dkind != XE_DM_LRU && ensure_dev(&m.d_tag, m.n_tag, m.pool_cap)) return -1;
+  if (ensure_dev(&m.d_tag, m.n_tag, m.pool_cap)) return -1;
+  if (m.dkind == XE_DM_LRU && dmemset(m.d_tag, 0, uint64_t(m.pool_cap) * 8, st)) return -1;  // no touches yet
   if (!m.d_hdr && dev_alloc((void**)&m.d_hdr, 8 * 8)) return -1;
   if (h2d(m.d_hdr, hdr.data(), 64, st) || dsync(st)) return -1;
   m.host_dirty = false;
@@ -1661,32 +1667,79 @@ static bool has_callbpf(const xe_vm* vm) {
   return false;
 }
 // The ordered maps a parallel run can serve: QUEUE / STACK pushes and PERF outputs (appends, put in
-// packet order after the run); any other operation on them (pops, peeks, lookups, every LRU_HASH
-// operation) raises XE_FLAG_ORDERED and the batch replays in packet order. LRU maps: straight away.
-static bool ordered_parallel_ok(const xe_vm* vm) {
-  for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].dkind == XE_DM_LRU) return false;
-  return true;
-}
-// the ordered maps' header words (counts, next ids, event bytes) at the start of a parallel run
+// packet order after the run) and LRU_HASH lookups (promotions, applied by last touch after the run);
+// any other operation on them (pops, peeks, list / event lookups, LRU updates and deletes) raises
+// XE_FLAG_ORDERED and the batch replays in packet order.
+static bool ordered_parallel_ok(const xe_vm*) { return true; }
+// the ordered maps' header words (counts, next ids, event bytes) at the start of a parallel run, and
+// the LRU maps' value pools (a parallel run adds into looked-up values in place)
 static int ordered_hdr_read(xe_vm* vm, std::vector<uint64_t>& out, xe_stream_t s) {
   out.assign(vm->maps.size() * 8, 0);
-  for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].ordered() && d2h(&out[i * 8], vm->maps[i].d_hdr, 64, s)) return -1;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (m.ordered() && d2h(&out[i * 8], m.d_hdr, 64, s)) return -1;
+    if (m.dkind == XE_DM_LRU) {
+      const uint64_t vb = uint64_t(m.pool_cap) * m.def.value_size;
+      if (ensure_dev(&m.d_vsnap, m.n_vsnap, vb) || (vb && d2d(m.d_vsnap, m.d_vals, vb, s))) return -1;
+    }
+  }
   return dsync(s);
 }
+// back to the headers of a parallel run's start; the LRU maps' touches of the run are dropped
 static int ordered_hdr_restore(xe_vm* vm, const std::vector<uint64_t>& h, xe_stream_t s) {
-  for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].ordered() && h2d(vm->maps[i].d_hdr, &h[i * 8], 64, s)) return -1;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (m.ordered() && h2d(m.d_hdr, &h[i * 8], 64, s)) return -1;
+    if (m.dkind == XE_DM_LRU && m.d_tag && dmemset(m.d_tag, 0, uint64_t(m.pool_cap) * 8, s)) return -1;
+    const uint64_t vb = uint64_t(m.pool_cap) * m.def.value_size;
+    if (m.dkind == XE_DM_LRU && vb && d2d(m.d_vals, m.d_vsnap, vb, s)) return -1;
+  }
   return dsync(s);
 }
+// The promotions of a parallel run's LRU lookups: in packet order every touched key ends up ahead of
+// the untouched ones, the most recently touched first (maps_hash_lru.go:51-68 per lookup). The run left
+// each value's last touch in its tag; the UsageList (device links) is rebuilt from them and the tags
+// are cleared for the next run.
+static int lru_finalize(xe_vm* vm, HostMap& m, xe_stream_t s) {
+  const uint32_t pool = m.pool_cap;
+  std::vector<uint64_t> tag(pool);
+  if (pool && (d2h(tag.data(), m.d_tag, uint64_t(pool) * 8, s) || dsync(s))) return -1;
+  std::vector<std::pair<uint64_t, uint32_t>> touched;
+  for (uint32_t v = 0; v < pool; v++)
+    if (tag[v]) touched.push_back({tag[v], v});
+  if (touched.empty()) return 0;
+  std::vector<uint64_t> hdr(8);
+  std::vector<uint32_t> link(4 * uint64_t(pool));
+  if (d2h(hdr.data(), m.d_hdr, 64, s) || d2h(link.data(), m.d_link, link.size() * 4, s) || dsync(s)) return -1;
+  std::vector<uint32_t> order;
+  order.reserve(hdr[2]);
+  std::sort(touched.begin(), touched.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  for (const auto& t : touched) order.push_back(t.second);
+  for (uint32_t v = uint32_t(hdr[0]); v != XE_NONE && order.size() <= hdr[2] + touched.size(); v = link[4 * uint64_t(v) + 1])
+    if (!tag[v]) order.push_back(v);
+  for (size_t i = 0; i < order.size(); i++) {
+    link[4 * uint64_t(order[i])] = i ? order[i - 1] : XE_NONE;
+    link[4 * uint64_t(order[i]) + 1] = i + 1 < order.size() ? order[i + 1] : XE_NONE;
+  }
+  hdr[0] = order.empty() ? XE_NONE : order.front();
+  hdr[1] = order.empty() ? XE_NONE : order.back();
+  if (h2d(m.d_link, link.data(), link.size() * 4, s) || h2d(m.d_hdr, hdr.data(), 64, s) ||
+      dmemset(m.d_tag, 0, uint64_t(pool) * 8, s) || dsync(s))
+    return -1;
+  return 0;
+}
+
 // put the appends of a parallel run (header words `h0` before it) into packet order
 static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t n, xe_stream_t s) {
   std::vector<uint64_t> h1;
   if (ordered_hdr_read(vm, h1, s)) return -1;
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
-    if (!m.ordered() || m.dkind == XE_DM_LRU) continue;
+    if (m.dkind == XE_DM_LRU) {
+      if (lru_finalize(vm, m, s)) return -1;
+      continue;
+    }
+    if (!m.ordered()) continue;
     const bool perf = m.dkind == XE_DM_PERF;
     const uint64_t base = perf ? h0[i * 8] : h0[i * 8 + 2];
     const uint64_t k = (perf ? h1[i * 8] : h1[i * 8 + 2]) - base;
@@ -1710,6 +1763,40 @@ static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t
       return -1;
   }
   return dsync(s);
+}
+
+// After a parallel pass that ran out of an ordered map's device room (header words h0 before it):
+// restore the headers, bring the host mirror to the batch's start and rebuild the device copies with
+// room for twice what the pass tried to append. 1: grown, 0: no ordered map was short, < 0: error.
+static int ordered_grow(xe_vm* vm, const std::vector<uint64_t>& h0, xe_stream_t s) {
+  std::vector<uint64_t> h1;
+  if (ordered_hdr_read(vm, h1, s)) return -1;
+  bool short_room = false;
+  uint64_t slack = vm->ord_slack, bytes = vm->ord_slack_bytes;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    const HostMap& m = vm->maps[i];
+    if (m.dkind == XE_DM_PERF) {
+      const uint64_t ev = h1[i * 8] - h0[i * 8], by = h1[i * 8 + 1] - h0[i * 8 + 1];
+      short_room = short_room || h1[i * 8] > m.pool_cap || h1[i * 8 + 1] > m.data_cap;
+      slack = std::max<uint64_t>(slack, 2 * ev + 4096);
+      bytes = std::max<uint64_t>(bytes, 2 * by + (1 << 20));
+    } else if (m.dkind == XE_DM_LIST) {
+      const uint64_t k = h1[i * 8 + 2] - h0[i * 8 + 2];
+      short_room = short_room || h1[i * 8 + 2] > m.pool_cap || h1[i * 8 + 1] > m.list_cap;
+      slack = std::max<uint64_t>(slack, 2 * k + 4096);
+    }
+  }
+  if (!short_room) return 0;
+  if (ordered_hdr_restore(vm, h0, s)) return -1;
+  vm->ord_slack = slack;
+  vm->ord_slack_bytes = bytes;
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (!m.ordered()) continue;
+    m.dev_dirty = true;  // the device copy (at the batch's start again) is the current state
+    if (map_download(vm, m) || ordered_upload(vm, m, vm->ord_slack, vm->ord_slack_bytes)) return -1;
+  }
+  return 1;
 }
 
 static bool has_ordered_maps(const xe_vm* vm) {
@@ -2216,15 +2303,30 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     void* pj = (jit && !P.results && !P.regs) ? lean_kernel(vm, jit) : jit;  // verdicts only: the lean variant
     vm->last_grid = parallel_grid(vm, pj, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
-    if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
-    if (pj ? launch_jit(pj, &P, vm->last_grid, 256, s) : launch_interp(&P, vm->last_grid, 256, s))
-      return fail(vm, XE_ERR_DEVICE, "kernel launch");
-    vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
-    if (fold()) return fail(vm, XE_ERR_DEVICE, "replica fold");
-    if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
-    kms = Timer::ms(vm->t0, vm->t1);
-    const uint32_t flags = uint32_t(red[0]);
-    conflict = run_conflict(red, P.nmaps);
+    uint32_t flags = 0;
+    for (int attempt = 0;; attempt++) {
+      if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
+      if (pj ? launch_jit(pj, &P, vm->last_grid, 256, s) : launch_interp(&P, vm->last_grid, 256, s))
+        return fail(vm, XE_ERR_DEVICE, "kernel launch");
+      vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
+      if (fold()) return fail(vm, XE_ERR_DEVICE, "replica fold");
+      if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
+      kms = Timer::ms(vm->t0, vm->t1);
+      flags = uint32_t(red[0]);
+      conflict = run_conflict(red, P.nmaps);
+      // appends past an ordered map's device room: the atomics counted every attempted append, so the
+      // room grows to what the batch needs and the parallel pass runs once more
+      if (ordmaps && attempt == 0 && (flags & XE_FLAG_CAPACITY) && !(flags & XE_FLAG_ORDERED)) {
+        const int g = ordered_grow(vm, ord_h0, s);
+        if (g < 0) return fail(vm, XE_ERR_DEVICE, "ordered map room");
+        if (g == 1) {
+          if (rollback(false) || prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+          P.maps = vm->d_maps;
+          continue;
+        }
+      }
+      break;
+    }
     if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
       // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the
       // keyed path, everything else (and what the keyed path refuses) the replay in packet order

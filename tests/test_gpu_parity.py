@@ -80,13 +80,13 @@ def test_device_resident_api_verdicts_only(gpu_lib, oracle_lib, name):
     st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n, d_verdicts=d_ver.data_ptr())
     torch.cuda.synchronize()
     ver = d_ver.cpu().numpy().view(np.uint32)
-    dev_map = vm.map_dump(1)
+    dev_map = vm.map_dump(1) if name != "c4" else None  # C4 has no map
     vm.close()
     ov = VM(Settings(), lib=oracle_lib)
     W.setup_vm(ov, name)
     r = ov.run_batch(umem.copy(), descs)
     assert (ver == r.verdicts).all()
-    if name != "c4":  # C4 has no map
+    if dev_map is not None:
         om = ov.map_dump(1)
         assert (np.array_equal(dev_map[0], om[0]) and np.array_equal(dev_map[1], om[1])) if isinstance(om, tuple) else dev_map == om
     assert st["steps"] == r.stats["steps"]

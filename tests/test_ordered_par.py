@@ -1,5 +1,8 @@
 """Ordered maps in parallel: QUEUE / STACK pushes and PERF_EVENT_ARRAY outputs run in parallel lanes and
-are put into packet order afterwards (xe_interp.h list_push_par, xe_runtime.cpp ordered_finalize).
+are put into packet order afterwards (xe_interp.h list_push_par, xe_runtime.cpp ordered_finalize); LRU_HASH
+lookups record each value's last touch and the UsageList is rebuilt from it (xe_runtime.cpp lru_finalize:
+in the reference every Lookup promotes, emulator/maps_hash_lru.go:51-91, so the final list is the touched
+keys by last touch, ahead of the untouched ones in their old order).
 
 The reference appends in its packet-by-packet loop (emulator/vm.go:110-173): QueueMap/StackMap.Push
 (emulator/maps_queue.go:60-77, maps_stack.go:60-77) and PerfEventArray.Push
@@ -11,7 +14,8 @@ import numpy as np
 import pytest
 
 from gobpfld_amd.asm import JEQ, JGT, JNE, Asm
-from gobpfld_amd.emulator import MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_PARALLEL, MODE_SEQUENTIAL, MapDef
+from gobpfld_amd.emulator import (MAP_LRU_HASH, MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_PARALLEL, MODE_SEQUENTIAL,
+                                  MapDef)
 from parity import assert_same, packets, run_one
 
 
@@ -54,6 +58,26 @@ def prog_perf():
     return a.assemble()
 
 
+def prog_lru(update=False):
+    """key = packet[0] % 64: look it up in an LRU_HASH (a hit promotes it) and add 1 to the value;
+    update: a miss inserts the key (an order-dependent write: eviction order)."""
+    a = Asm()
+    _head(a, 16)
+    a.ldx(1, 3, 6, 0).alu64(0x50, 3, 63).stx(4, 10, -4, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "miss", imm=0)
+    a.mov64(1, 1).xadd(8, 0, 0, 1)
+    a.ja("out")
+    a.label("miss")
+    if update:
+        a.st(8, 10, -16, 7).ld_map(1, 1).mov64(2, src=10).add64(2, -4).mov64(3, src=10).add64(3, -16)
+        a.mov64(4, 0).call(2)
+    a.label("out").mov64(0, 2).exit()
+    return a.assemble()
+
+
+LRU = (MapDef(MAP_LRU_HASH, 4, 8, 64), None)
+LRU_PRELOAD = {0: [(k.to_bytes(4, "little"), (1000 * k).to_bytes(8, "little")) for k in range(0, 96, 2)]}
 QUEUE = (MapDef(MAP_QUEUE, 0, 8, 16), None)
 STACK = (MapDef(MAP_STACK, 0, 8, 16), None)
 PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
@@ -64,6 +88,8 @@ CASES = {
     "stack": (prog_push, STACK, PRELOAD, MODE_PARALLEL),
     "perf": (prog_perf, PERF, None, MODE_PARALLEL),
     "queue_pop": (lambda: prog_push(pop=True), QUEUE, PRELOAD, MODE_SEQUENTIAL),
+    "lru_lookup": (prog_lru, LRU, LRU_PRELOAD, MODE_PARALLEL),
+    "lru_update": (lambda: prog_lru(update=True), LRU, LRU_PRELOAD, MODE_SEQUENTIAL),
 }
 
 
@@ -83,7 +109,7 @@ def test_appends_hostsim_equal_oracle(oracle_lib, hostsim_lib, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_appends_device_equal_oracle(gpu_lib, oracle_lib, name):
-    n = 4096 if name == "queue_pop" else 262144
+    n = 4096 if name in ("queue_pop", "lru_update") else 262144
     got = _run(gpu_lib, name, n)
     assert_same(got, _run(oracle_lib, name, n), name)
     assert got[0].stats["mode_used"] == CASES[name][3]

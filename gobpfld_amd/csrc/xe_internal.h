@@ -238,7 +238,7 @@ XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
 #define XE_KINS 2u            // ikey slots per packet (more held-back inserts: the one-lane replay)
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
 enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
-                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW };
+                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW, XE_KS_CFLAG, XE_KS_CLIST };
 // Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
 // a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
 // a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
@@ -249,6 +249,8 @@ enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_
 #define XE_KS_CHANGED 65                    // union-find round changed something
 #define XE_KS_NO 66                         // packets on chains
 #define XE_KS_LONG 67                       // some chain holds more than half the batch
+#define XE_KS_NCH 68                        // chains (the compacted chain list's length)
+#define XE_KS_CNEXT 69                      // the chain pass's work queue: next unclaimed chain
 #define XE_KS_CINS 128                      // [64 maps][XE_KSTRIPES] inserts the chains made
 #define XE_KS_WORDS (128 + 64 * XE_KSTRIPES)
 #define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid
@@ -273,7 +275,7 @@ struct XeKeyed {
   uint32_t* okey;      // [n] sorted chain keys
   uint32_t* order;     // [n] packet indices sorted by chain, in packet order within a chain
   uint32_t* iota;      // [n] 0..n-1 (sort input)
-  uint32_t* counts;    // [0] packets on chains (nO)
+  uint32_t* counts;    // [0] packets on chains (nO), [1] a long chain, [2] chains, [3] the chain pass's queue
   const uint8_t* skip; // [n] 1 = the packet runs on a chain (the parallel pass leaves it out)
   uint32_t n;          // packets of the batch
   uint32_t nO;         // packets on chains: order[0..nO) (a chain starts where the sorted key changes)

@@ -3018,6 +3018,15 @@ XE_DEV void keyed_clong_item(const XeKeyed& K, uint32_t p) {
   if (p + 1 < K.nO && K.okey[p + 1] == K.okey[p]) return;  // not a chain's last packet
   if (uint64_t(p + 1 - K.cstart[K.okey[p]]) * 2 > K.n) K.counts[1] = 1;
 }
+// the compacted chain list: iota[p] = 1 where a chain starts, an exclusive scan of it into ckey, then
+// cstart[ckey[p]] = p (cstart is free again once the long-chain check has run) and the chain count
+XE_DEV void keyed_cflag_item(const XeKeyed& K, uint32_t p) {
+  K.iota[p] = (p == 0 || K.okey[p] != K.okey[p - 1]) ? 1u : 0u;
+}
+XE_DEV void keyed_clist_item(const XeKeyed& K, uint32_t p) {
+  if (K.iota[p]) K.cstart[K.ckey[p]] = p;
+  if (p + 1 == K.nO) K.counts[2] = K.ckey[p] + K.iota[p];
+}
 XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t i) {
   switch (step) {
     case XE_KS_DSET: keyed_dset_item(K, i); break;
@@ -3030,45 +3039,59 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_CSTART: keyed_cstart_item(K, i); break;
     case XE_KS_CLONG: keyed_clong_item(K, i); break;
     case XE_KS_UNNEW: keyed_unnew_item(K, maps, i); break;
+    case XE_KS_CFLAG: keyed_cflag_item(K, i); break;
+    case XE_KS_CLIST: keyed_clist_item(K, i); break;
     default: break;
   }
 }
 
-// Chain-mode driver (XE_MODE_CHAIN, keyed ordered execution): thread g of the grid looks at sorted
-// positions g, g + nthreads, ... and runs the chain starting at each position where the sorted chain
-// key changes, its packets in packet order (order[p..] while the key stays the same). All lanes of a
-// wave call body together until every lane of the wave has run out of positions.
+// Chain-mode driver (XE_MODE_CHAIN, keyed ordered execution): the chains (cstart[0..nch): first
+// positions in the sorted order; a chain's packets are order[p..] while the sorted key stays the same)
+// are a work queue. A wave claims XE_WAVE chain indices at a time (one atomic on counts[3]); every lane
+// that has finished its chain takes the next unassigned index of the wave's claim, so a lane with a
+// short chain goes on to another instead of idling until the wave's longest chain ends. All lanes of a
+// wave call body together until the queue is empty and every lane is done.
 template <class Body>
 XE_DEV void chain_packets(XeLane& L, const XeParams& P, uint32_t g, uint32_t nthreads, Body body) {
-  uint32_t q = g, p = 0, key = 0;  // q: the lane's next candidate start position (grid-stride)
+  (void)g;
+  (void)nthreads;
+  const uint32_t nch = xe_load_relaxed32(P.K.counts + 2);
+  uint32_t qn = 0, qe = 0;  // wave-uniform: the wave's claimed chain indices not yet handed out
+  bool drained = false;     // wave-uniform: the queue has no chains left
+  uint32_t p = 0, pend = 0, key = 0;
   bool have = false;
-  auto next_chain = [&]() {
-    have = false;
-#pragma unroll 1
-    while (q < P.K.nO) {
-      const uint32_t c = q;
-      q += nthreads;
-      if (c == 0 || P.K.okey[c] != P.K.okey[c - 1]) {
-        p = c;
-        key = P.K.okey[c];
-        have = true;
-        break;
-      }
-    }
-  };
-  next_chain();
 #pragma unroll 1
   for (;;) {
-    if (!xe_ballot(have)) break;
+    const uint64_t idle = xe_ballot(!have);
+    if (idle && qn >= qe && !drained) {
+      uint32_t base = 0;
+      if (xe_lane() == __builtin_ctzll(idle)) base = xe_atomic_add32(P.K.counts + 3, uint32_t(XE_WAVE));
+      base = uint32_t(xe_readlane(int(base), int(__builtin_ctzll(idle))));
+      if (base >= nch) drained = true;
+      else { qn = base; qe = base + XE_WAVE < nch ? base + XE_WAVE : nch; }
+    }
+    if (idle && qn < qe) {
+      const uint32_t rank = uint32_t(__builtin_popcountll(idle & xe_lanemask_lt()));
+      if (!have && qn + rank < qe) {
+        const uint32_t c = qn + rank;
+        p = P.K.cstart[c];
+        pend = c + 1 < nch ? P.K.cstart[c + 1] : P.K.nO;
+        key = P.K.okey[p];
+        have = true;
+      }
+      const uint32_t given = uint32_t(__builtin_popcountll(idle));
+      qn = qn + given < qe ? qn + given : qe;
+    }
+    if (!xe_ballot(have)) {
+      if (drained) break;
+      continue;
+    }
     const uint32_t i = have ? P.K.order[p] : 0u;
     L.kchain = key;
     lane_reset(L, P, i, have);
     key_begin(L, i);
     body(i, have);
-    if (have) {
-      p++;
-      if (p >= P.K.nO || P.K.okey[p] != key) next_chain();
-    }
+    if (have && ++p >= pend) have = false;
   }
 }
 #endif

@@ -8,6 +8,7 @@
 #include "xe_interp.h"
 
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
 
 extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t hdr_lds[XE_HDR_LDS_BYTES];
@@ -275,6 +276,19 @@ extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* s
     return -1;
   hipLaunchKernelGGL(xe_append_kernel, dim3(blocks), dim3(256), 0, s, *A, 1);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// exclusive scan of the chain-start flags (iota) into ckey: each chain's index in the compacted list
+extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s) {
+  size_t tmp = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, int(n), s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *bytes = tmp;
+    return 0;
+  }
+  if (*bytes < tmp) return -1;
+  return hipcub::DeviceScan::ExclusiveSum(scratch, tmp, K->iota, K->ckey, int(n), s) == hipSuccess ? 0 : -1;
 }
 
 // host-side launchers (called from xe_runtime.cpp)

@@ -42,6 +42,7 @@ extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* 
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -195,6 +196,12 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, siz
   for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
   return 0;
 }
+int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t) {
+  if (!scratch) { *bytes = 8; return 0; }
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < n; i++) { K->ckey[i] = acc; acc += K->iota[i]; }
+  return 0;
+}
 int launch_append(const XeAppendArgs* A, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
   if (!scratch) { *bytes = 8; return 0; }
   std::vector<std::pair<uint64_t, uint32_t>> v(A->k);
@@ -257,6 +264,9 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scra
 }
 int launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
   return xe_launch_append(A, end_bit, scratch, bytes, s);
+}
+int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t s) {
+  return xe_launch_keyed_scan(K, n, scratch, bytes, s);
 }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
@@ -2245,7 +2255,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (general && ensure_arena(vm, false, pgrid * 256, Y.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
       if (launch(&Y, pgrid, 256) || fold()) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed parallel)");
     }
-    // 5. the chains, one lane each, in packet order
+    // 5. the chains in packet order: the compacted chain list is a work queue the waves claim from
+    {
+      size_t sb2 = 0;
+      if (step(XE_KS_CFLAG, K.nO) || launch_keyed_scan(&K, K.nO, nullptr, &sb2, s) ||
+          ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb2) || launch_keyed_scan(&K, K.nO, vm->d_ksort, &sb2, s) ||
+          step(XE_KS_CLIST, K.nO) || dmemset(vm->d_ksmall + XE_KS_CNEXT, 0, 4, s))
+        return fail(vm, XE_ERR_DEVICE, "keyed chain list");
+    }
     X.mode = XE_MODE_CHAIN;
     X.K.skip = nullptr;
     const uint32_t cgrid = std::max<uint32_t>(1, std::min<uint32_t>(grid, (K.nO + 255) / 256));

@@ -53,10 +53,10 @@ ISSUE_PEAK = 256 * 64 * 2.4e9  # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz (SU
 
 
 def pmc_traffic(name: str, n: int) -> tuple[float | None, str | None]:
-    """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE corrected
-    per access shape + WRITE_SIZE; profiles/r2/final/<config>_traffic.json, made by
-    scripts/traffic_final.py), when one exists for this exact batch size; else (None, None)."""
-    for rnd in ("r2/final", "r2", "r1"):  # newest committed PMC passes first
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload (2 x FETCH_SIZE +
+    WRITE_SIZE, MI355X_MICROARCH.md; profiles/r3/<config>_traffic.json, made by scripts/traffic_r3.py),
+    when one exists for this exact batch size; else (None, None)."""
+    for rnd in ("r3", "r2/final"):  # newest committed PMC passes first
         f = ROOT / "profiles" / rnd / f"{name}_traffic.json"
         if f.exists():
             break

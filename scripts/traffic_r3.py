@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the emulator kernel for C2-C5 from the round-3 PMC passes
+(scripts/gpu_r3_pmc.sh: separate rocprofv3 --pmc runs of FETCH_SIZE, WRITE_SIZE and
+TCC_EA0_RDREQ_sum + TCC_EA0_ATOMIC_sum over `bench.py --config <c> --steps 5`).
+
+  python scripts/traffic_r3.py <pmc dir (gpurun_out/r3pmc)> <out dir (profiles/r3)>
+
+Correction as MI355X_MICROARCH.md prescribes (HBM/rocprofv3 section): on gfx950 FETCH_SIZE reports half
+of the bytes of wide coalesced streaming reads, so `hbm_bytes_per_launch` = 2 x FETCH_SIZE + WRITE_SIZE.
+That is exact for the streaming parts (descriptors, back-to-back header windows) and an upper bound for
+the random 64-B hash probe groups, which the round-2 calibration (tools/calib_fetch*.hip,
+profiles/r2/fetch_size_calibration*.json) found counted at x1; `bounds_x1_x2` gives both ends.
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+from pathlib import Path
+
+PKTS = {"c2": 16777216, "c3": 16777216, "c4": 16777216, "c5": 33554432}
+
+
+def per_launch(d: Path) -> dict:
+    f = glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=True)[0]
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        if r["Kernel_Name"].startswith("xe_jit_kernel"):
+            acc[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = collections.defaultdict(float)
+    for k in acc:
+        for c, v in acc[k].items():
+            out[c] += v / len(acc)
+    return dict(out) | {"dispatches": len(acc)}
+
+
+def main() -> None:
+    src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+    dst.mkdir(parents=True, exist_ok=True)
+    for name, n in PKTS.items():
+        fetch = per_launch(src / f"{name}_fetch")["FETCH_SIZE"] * 1024
+        write = per_launch(src / f"{name}_write")["WRITE_SIZE"] * 1024
+        rq = per_launch(src / f"{name}_rdreq")
+        alg = 84 * n
+        hbm = 2 * fetch + write
+        d = {
+            "workload": name, "packets": n, "kernel": "xe_jit_kernel", "dispatches": rq["dispatches"],
+            "fetch_size_bytes_raw": round(fetch), "write_size_bytes": round(write),
+            "tcc_ea0_rdreq": round(rq["TCC_EA0_RDREQ_sum"]), "tcc_ea0_atomic": round(rq["TCC_EA0_ATOMIC_sum"]),
+            "per_packet": {"fetch_raw": round(fetch / n, 1), "write": round(write / n, 1),
+                           "rdreq": round(rq["TCC_EA0_RDREQ_sum"] / n, 3),
+                           "memory_side_atomics": round(rq["TCC_EA0_ATOMIC_sum"] / n, 3)},
+            "hbm_bytes_per_launch": round(hbm),
+            "hbm_bytes_per_packet": round(hbm / n, 1),
+            "bounds_x1_x2": [round(fetch + write), round(hbm)],
+            "alg_bytes_per_launch": alg,
+            "traffic_over_alg": round(hbm / alg, 3),
+            "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE reports half of wide streaming reads)",
+            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ_sum,TCC_EA0_ATOMIC_sum, separate passes of "
+                      f"python3 bench.py --config {name} --packets {n} --steps 5 --warmup 1 (scripts/gpu_r3_pmc.sh)",
+        }
+        (dst / f"{name}_traffic.json").write_text(json.dumps(d, indent=1) + "\n")
+        print(name, d["per_packet"], "hbm/pkt", d["hbm_bytes_per_packet"], "ratio", d["traffic_over_alg"])
+
+
+if __name__ == "__main__":
+    main()

@@ -59,7 +59,19 @@ def main() -> None:
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ_sum,TCC_EA0_ATOMIC_sum, separate passes of "
                       f"python3 bench.py --config {name} --packets {n} --steps 5 --warmup 1 (scripts/gpu_r3_pmc.sh)",
         }
+        # the round-2 shape calibration (profiles/r2/fetch_size_calibration*.json): streaming parts x2,
+        # random probe groups x1, 1500-B-stride windows counted at 0.82 of the 64-B blocks they touch
+        if name in ("c2", "c5"):
+            cal = fetch + 40 * n  # descriptors + back-to-back windows stream (counted half); probes x1
+        elif name == "c4":
+            cal = 16 * n + (fetch - 8 * n) / (385.0e6 / 469.8e6)
+        else:
+            cal = fetch + 8 * n  # IMIX: descriptors stream; windows and probes at x1 (a lower bound)
+        d["calibrated_estimate"] = {"hbm_bytes_per_packet": round((cal + write) / n, 1),
+                                    "traffic_over_alg": round((cal + write) / alg, 3),
+                                    "model": "round-2 per-shape calibration of FETCH_SIZE (scripts/traffic_final.py)"}
         (dst / f"{name}_traffic.json").write_text(json.dumps(d, indent=1) + "\n")
+        print(name, "calibrated", d["calibrated_estimate"])
         print(name, d["per_packet"], "hbm/pkt", d["hbm_bytes_per_packet"], "ratio", d["traffic_over_alg"])
 
 

@@ -55,10 +55,20 @@ __global__ void xe_sum_kernel(C* acc, const C* in, uint64_t n) {
 }
 
 // vals += sum of the replicas; replicas := 0 (only words that received adds are written). All nrep
-// loads are issued before any store so they overlap (no store may alias a later load).
+// loads are issued before any store so they overlap (no store may alias a later load). HASH maps (recs != nullptr): only the words of slots that
+// hold or held an entry (slot state != 0) — a replica of a never-used slot is zero, since a map add
+// needs a value pointer and a lookup only returns one for a full slot — so a large, sparsely filled
+// table folds its replicas at the cost of one slot-state read per value word.
 extern "C" __global__ void xe_rep_fold_kernel(unsigned long long* __restrict__ vals, unsigned long long* __restrict__ rep,
-                                              uint64_t stride_words, uint32_t nrep, uint64_t nwords) {
+                                              uint64_t stride_words, uint32_t nrep, uint64_t nwords,
+                                              const unsigned long long* __restrict__ recs, uint32_t rwords, uint32_t vsize,
+                                              uint32_t cap) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x) {
+    if (recs) {
+      const uint64_t s0 = 8 * i / vsize, s1 = (8 * i + 7) / vsize;
+      const bool live = (s0 <= cap && recs[s0 * rwords] != 0) || (s1 != s0 && s1 <= cap && recs[s1 * rwords] != 0);
+      if (!live) continue;
+    }
     unsigned long long v[16];
 #pragma unroll
     for (uint32_t k = 0; k < 16; k++) v[k] = k < nrep ? rep[k * stride_words + i] : 0ull;
@@ -371,10 +381,11 @@ extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, cons
   }
   return 0;
 }
-extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s) {
+extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords,
+                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, hipStream_t s) {
   uint32_t blocks = uint32_t(nwords / 256 + 1);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(xe_rep_fold_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)vals, (unsigned long long*)rep,
-                     stride_words, nrep, nwords);
+                     stride_words, nrep, nwords, (const unsigned long long*)recs, rwords, vsize, cap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -29,7 +29,8 @@ extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t thr
 extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane,
                                      hipStream_t s);
-extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords, hipStream_t s);
+extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords,
+                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, hipStream_t s);
 extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
@@ -128,11 +129,18 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
   for (uint32_t g = 0; g < nseg; g++) memcpy(dst[g], src[g], words[g] * 8);
   return 0;
 }
-int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t) {
+int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t nw, const void* recs, uint32_t rwords,
+                    uint32_t vsize, uint32_t cap, xe_stream_t) {
   uint64_t* v = (uint64_t*)vals;
   uint64_t* r = (uint64_t*)rep;
-  for (uint64_t i = 0; i < nw; i++)
+  const uint64_t* rc = (const uint64_t*)recs;
+  for (uint64_t i = 0; i < nw; i++) {
+    if (rc) {  // xe_kernel.hip xe_rep_fold_kernel: only the words of slots that hold or held an entry
+      const uint64_t s0 = 8 * i / vsize, s1 = (8 * i + 7) / vsize;
+      if (!((s0 <= cap && rc[s0 * rwords]) || (s1 != s0 && s1 <= cap && rc[s1 * rwords]))) continue;
+    }
     for (uint32_t k = 0; k < nrep; k++) { v[i] += r[k * sw + i]; r[k * sw + i] = 0; }
+  }
   return 0;
 }
 int launch_tail(const XeTailArgs* A, xe_stream_t) {  // xe_kernel.hip xe_tail_kernel, one thread
@@ -247,7 +255,10 @@ int launch_delta(const void* c, const void* sn, void* o, uint64_t b, uint32_t la
 int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t b, uint32_t lane, xe_stream_t s) {
   return xe_launch_apply_delta(c, sn, d, b, lane, s);
 }
-int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, xe_stream_t s) { return xe_launch_rep_fold(v, r, sw, nrep, nw, s); }
+int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, const void* recs, uint32_t rwords, uint32_t vsize,
+                    uint32_t cap, xe_stream_t s) {
+  return xe_launch_rep_fold(v, r, sw, nrep, nw, recs, rwords, vsize, cap, s);
+}
 int launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, xe_stream_t s) {
   return xe_launch_delta_sum(acc, in, bytes, lane, s);
 }
@@ -859,11 +870,21 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 // to run, 4: 1.08 ms, 16: 1.05-1.09 ms over 6 VM placements); C5 (1M uniform flows) is fastest with
 // none (3.45 ms; each doubling costs ~5 %). The bound once sat at exactly 128 MB, which the region's
 // extra empty-key slot pushed C3 past (2 replicas, the bimodal case).
-uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc) {
+// HASH maps fold only their used slots (fold_map), so their bound is on the live bytes: C3's 64K hot
+// flows get 16 replicas (4 had a slow mode in 3 of 10 fresh processes: 2.13 ms against 1.0 ms,
+// profiles/r3/c3_modes.json); an ARRAY folds its whole region.
+uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc, bool hash) {
   if (const char* e = xe_tuning_env("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));
   uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
-  while (want > 1 && uint64_t(want) * vals_alloc > (160ull << 20)) want >>= 1;
+  while (want > 1 && uint64_t(want) * (hash ? live : vals_alloc) > (160ull << 20)) want >>= 1;
   return want;
+}
+
+// vals += the replicas (replicas := 0); a HASH map only over the slots that hold or held an entry
+int fold_map(HostMap& m, xe_stream_t s) {
+  const bool hash = m.dkind == XE_DM_HASH && m.def.value_size > 0;
+  return launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, hash ? m.d_keys : nullptr,
+                         hash ? xe_hash_rwords(m.kwords) : 0, hash ? m.def.value_size : 8, m.cap, s);
 }
 
 int map_alloc_device(HostMap& m) {
@@ -1145,7 +1166,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       if (map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
     }
     const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
-    const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc) : 1u;
+    const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc, m.dkind == XE_DM_HASH) : 1u;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
       dev_free(m.d_rep);
       m.d_rep = nullptr;
@@ -2159,7 +2180,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   auto fold = [&]() -> int {
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
-      if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s)) return -1;
+      if (m.nrep > 1 && fold_map(m, s)) return -1;
     }
     return 0;
   };
@@ -2605,7 +2626,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   sl.t1.rec(s);
   for (size_t i : big) {
     HostMap& m = vm->maps[i];
-    if (m.nrep > 1 && launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, s))
+    if (m.nrep > 1 && fold_map(m, s))
       return fail(vm, XE_ERR_DEVICE, "replica fold");
   }
   if (launch_tail(&A, s)) return fail(vm, XE_ERR_DEVICE, "epilogue");

@@ -1096,15 +1096,23 @@ XE_DEV void hdr_write(XeLane& L, int off, int size, uint64_t x) {
   for (int b = 0; b < size; b++) *hdr_at(L, off + L.hsh + b) = uint8_t(x >> (8 * b));
 }
 
-// packet ByteMemory access through the header window when possible
+// packet ByteMemory access through the header window when possible. A per-program kernel's
+// XE_HDR_LO is the least offset its packet-read analysis proved for any read (XE_HDR_LO_PROVEN), so a
+// load needs no lower-bound test there; stores are not part of the analysis and keep it.
 XE_DEV bool in_window(const XeLane& L, int64_t off, int size) {
 #if XE_HDR_LO > 0
   if (off < XE_HDR_LO) return false;
 #endif
   return off + size <= L.hdr_len;
 }
+XE_DEV bool in_window_read(const XeLane& L, int64_t off, int size) {
+#if XE_HDR_LO > 0 && !defined(XE_HDR_LO_PROVEN)
+  if (off < XE_HDR_LO) return false;
+#endif
+  return off + size <= L.hdr_len;
+}
 XE_DEV uint64_t pkt_load(const XeLane& L, int64_t off, int size) {
-  if (in_window(L, off, size)) return hdr_read(L, int(off), size);
+  if (in_window_read(L, off, size)) return hdr_read(L, int(off), size);
   uint64_t x = load_le(L.pkt + off, size);
   xe_pin(x);  // wait here, on the rare path, not at the join (where it would drain the prefetch)
   return x;

@@ -72,6 +72,29 @@ ncclDataType_t container_type(uint32_t lane) {
 // delta containers of a map whose value region is `bytes` long, in lanes of `lane`
 uint64_t delta_bytes(uint64_t bytes, uint32_t lane) { return lane == 2 ? 2 * bytes : bytes; }
 
+// buf[k][mi - 1] := the sum over k of the VMs' deltas of map mi (vb value bytes, db container bytes)
+int reduce_sum(xe_multi* m, int mi, uint32_t lane, uint64_t vb, uint64_t db) {
+  const size_t G = m->vms.size(), j = size_t(mi - 1);
+  if (m->rccl) {
+#ifndef XE_HOSTSIM
+    const size_t cnt = size_t(db / (lane == 8 ? 8 : lane == 1 ? 1 : 4));
+    if (ncclGroupStart() != ncclSuccess) return -1;
+    for (size_t k = 0; k < G; k++)
+      if (ncclAllReduce(m->buf[k][j], m->buf[k][j], cnt, container_type(lane), ncclSum, m->comms[k],
+                        (hipStream_t)xe_internal_vm_stream(m->vms[k])) != ncclSuccess)
+        return -1;
+    return ncclGroupEnd() == ncclSuccess ? 0 : -1;
+#else
+    return -1;
+#endif
+  }
+  for (size_t k = 1; k < G; k++)  // same device: accumulate into VM 0's buffer, then hand it to the rest
+    if (xe_internal_delta_sum(m->vms[0], m->buf[0][j], m->buf[k][j], vb, lane)) return -1;
+  for (size_t k = 1; k < G; k++)
+    if (xe_internal_copy(m->vms[k], m->buf[k][j], m->buf[0][j], db)) return -1;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -180,27 +203,12 @@ int xe_run_batch_multi(xe_multi* m, void* const* d_umem, const uint64_t* umem_le
         void* b = map_buf(k, mi, db);
         if (!b || xe_map_delta(m->vms[k], mi, lane, b, nullptr)) return mfail(m, XE_ERR_DEVICE, "map delta");
       }
-      if (m->rccl) {
-#ifndef XE_HOSTSIM
-        const size_t cnt = size_t(db / (lane == 8 ? 8 : lane == 1 ? 1 : 4));
-        if (ncclGroupStart() != ncclSuccess) return mfail(m, XE_ERR_DEVICE, "rccl group");
-        for (size_t k = 0; k < G; k++)
-          if (ncclAllReduce(m->buf[k][size_t(mi - 1)], m->buf[k][size_t(mi - 1)], cnt, container_type(lane), ncclSum,
-                            m->comms[k], (hipStream_t)xe_internal_vm_stream(m->vms[k])) != ncclSuccess)
-            return mfail(m, XE_ERR_DEVICE, "rccl all-reduce");
-        if (ncclGroupEnd() != ncclSuccess) return mfail(m, XE_ERR_DEVICE, "rccl group");
-        for (size_t k = 0; k < G; k++)
-          if (xe_map_apply_delta(m->vms[k], mi, lane, m->buf[k][size_t(mi - 1)], nullptr))
-            return mfail(m, XE_ERR_DEVICE, "apply delta");
-#endif
-      } else {
-        void* acc = m->buf[0][size_t(mi - 1)];
-        for (size_t k = 1; k < G; k++)
-          if (xe_internal_delta_sum(m->vms[0], acc, m->buf[k][size_t(mi - 1)], vb, lane))
-            return mfail(m, XE_ERR_DEVICE, "delta sum");
-        for (size_t k = 0; k < G; k++)
-          if (xe_map_apply_delta(m->vms[k], mi, lane, acc, nullptr)) return mfail(m, XE_ERR_DEVICE, "apply delta");
-      }
+      // sum the deltas into every VM's buffer: one RCCL all-reduce across distinct devices, device
+      // kernels when the VMs share one — the only line that differs between the two
+      if (reduce_sum(m, mi, lane, vb, db)) return mfail(m, XE_ERR_DEVICE, "delta all-reduce");
+      for (size_t k = 0; k < G; k++)
+        if (xe_map_apply_delta(m->vms[k], mi, lane, m->buf[k][size_t(mi - 1)], nullptr))
+          return mfail(m, XE_ERR_DEVICE, "apply delta");
     }
   } else {
     // ---- in-order replay: shard k starts from the state shard k-1 ended with

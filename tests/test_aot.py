@@ -34,6 +34,7 @@ def test_window_from_packet_read_range(hostsim_lib, name):
     srcs = aot.sources([_case(name)], lib=hostsim_lib)
     assert srcs, "no kernel source generated"
     assert _window(srcs[0]) == WINDOWS[name]
+    assert "#define XE_HDR_LO_PROVEN 1" in srcs[0]  # every read is at or above XE_HDR_LO
 
 
 def test_unbounded_packet_pointer_keeps_full_window(hostsim_lib):

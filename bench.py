@@ -37,6 +37,9 @@ WORKLOADS = {
                "map-entry writes, order-dependent; IMIX 64/576/1500 B",
     "c2rmw": "C2-RMW: C2 with the per-proto counter bumped by a plain load/add/store (value->packets++ without "
              "an atomic): the ordered read-modify-write, run in parallel through lift_rmw",
+    "bpf2bpf": "bpf2bpf: call-heavy analogue of the reference's cmd/examples/bpf_to_bpf/src/xdp.c — Ethernet / IPv4 "
+               "parse and two bpf-to-bpf calls per packet into a stats sub-program (lookup, lifted {pkts, bytes} "
+               "adds), 3 HASH maps, 64 B packets",
 }  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec peak
 
 

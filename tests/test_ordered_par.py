@@ -106,6 +106,16 @@ def test_appends_hostsim_equal_oracle(oracle_lib, hostsim_lib, name):
     assert got[0].stats["mode_used"] == CASES[name][3]
 
 
+@pytest.mark.parametrize("name", ["queue", "perf"])
+def test_appends_hostsim_past_device_room(oracle_lib, hostsim_lib, name):
+    """More appends than the device room a run starts with (xe_runtime.cpp ord_slack, 4096 elements /
+    events): the parallel pass counts every attempted append, ordered_grow resizes the device lists and
+    the pass runs once more — still PARALLEL, still the reference's list."""
+    got = _run(hostsim_lib, name, 6144)
+    assert_same(got, _run(oracle_lib, name, 6144), name)
+    assert got[0].stats["mode_used"] == MODE_PARALLEL
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_appends_device_equal_oracle(gpu_lib, oracle_lib, name):

@@ -5,10 +5,16 @@ Default workload (N=1) = BASELINE configs[1], "C2": ~40-insn L2/L3 classifier ov
 synthetic packets with per-proto ARRAY counters. A step = one pass of the batch through the emulator
 (a pipelined xe_run_batch_device_async: the per-program kernel, then the one-block epilogue with the
 device-side commutativity check; --sync: xe_run_batch_device) with packets, descriptors and the
-verdict buffer already resident in HBM. For N>1 (torchrun, one rank per GPU) every rank runs its own
-16M-packet shard (weak scaling); the timed steps form one shard epoch whose counter map deltas are
-all-reduced over RCCL (or replayed in order) inside the timed region. Prints ONE JSON line (rank 0)
-with roofline and cpu_baseline objects.
+verdict buffer already resident in HBM.
+
+N > 1: one process per GPU (torchrun; `--gpus N` without torchrun starts the same ranks as children),
+every rank runs its own 16M-packet shard (weak scaling) and the timed steps form one shard epoch whose
+map deltas are all-reduced over RCCL (or replayed in order) inside the timed region — the same code
+path for N = 1..8. After the timed region every rank checks its verdicts and its map against truth
+derived from the generated headers (`verified`). The default line also carries BASELINE configs[4]
+as the `c5` side line (33.5M packets per GPU, per-flow HASH counters, the per-flow delta exchange
+timed separately, verified the same way). Prints ONE JSON line (rank 0) with roofline and
+cpu_baseline objects.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--packets P]
 """
@@ -52,23 +58,45 @@ def alg_bytes_per_packet(name: str, sizes: np.ndarray) -> np.ndarray:
 
 
 ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
-ISSUE_PEAK = 256 * 64 * 2.4e9  # lane-ops/s: 256 CU x 64 lanes/clk x 2.4 GHz (SURVEY §8d issue roofline)
+
+
+PROFILE_ROUND = "r4"  # newest committed PMC passes (scripts/gpu_pmc.sh); earlier rounds' are superseded
+
+
+def _profile(name: str, kind: str, n: int) -> tuple[dict | None, str | None]:
+    """profiles/<round>/<config>_<kind>.json of this exact workload and batch size (newest round first)."""
+    for rnd in (PROFILE_ROUND, "r3"):
+        f = ROOT / "profiles" / rnd / f"{name}_{kind}.json"
+        if f.exists():
+            d = json.loads(f.read_text())
+            if d.get("workload") == name and int(d.get("packets", -1)) == n:
+                return d, str(f.relative_to(ROOT))
+            return None, None
+    return None, None
 
 
 def pmc_traffic(name: str, n: int) -> tuple[float | None, str | None]:
     """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload (2 x FETCH_SIZE +
-    WRITE_SIZE, MI355X_MICROARCH.md; profiles/r3/<config>_traffic.json, made by scripts/traffic_r3.py),
-    when one exists for this exact batch size; else (None, None)."""
-    for rnd in ("r3", "r2/final"):  # newest committed PMC passes first
-        f = ROOT / "profiles" / rnd / f"{name}_traffic.json"
-        if f.exists():
-            break
-    else:
-        return None, None
-    d = json.loads(f.read_text())
-    if d.get("workload") != name or int(d.get("packets", -1)) != n:
-        return None, None
-    return float(d["hbm_bytes_per_launch"]), str(f.relative_to(ROOT))
+    WRITE_SIZE, MI355X_MICROARCH.md; profiles/<round>/<config>_traffic.json), when one exists for this exact
+    batch size; else (None, None)."""
+    d, src = _profile(name, "traffic", n)
+    return (None, None) if d is None else (float(d["hbm_bytes_per_launch"]), src)
+
+
+def sq_issue(name: str, n: int, kernel_s: float | None = None) -> dict:
+    """Issue-slot use of the emulator kernel from the committed SQ counter pass of this workload
+    (profiles/<round>/<config>_sq_counters.json): wave-instructions per launch against one VALU and one
+    SALU issue per CU per clock (256 CUs x 2.4 GHz) over the live average kernel time. Replaces the old
+    eBPF-instructions-per-lane 'issue_frac', which counted emulated instructions, not machine issue."""
+    d, src = _profile(name, "sq_counters", n)
+    if d is None or not kernel_s:
+        return {"sq_issue": None}
+    slots = 256 * 2.4e9 * kernel_s
+    pl = d["per_launch"]
+    return {"sq_issue": {"valu_frac": round(pl["SQ_INSTS_VALU"] / slots, 4), "salu_frac": round(pl["SQ_INSTS_SALU"] / slots, 4),
+                         "valu_per_chunk": d["per_64_packet_chunk"]["SQ_INSTS_VALU"],
+                         "salu_per_chunk": d["per_64_packet_chunk"]["SQ_INSTS_SALU"],
+                         "wait_frac": round(pl["SQ_WAIT_INST_ANY"] / max(1, pl["SQ_WAVE_CYCLES"]), 4), "source": src}}
 
 
 def _oracle_prep(name: str, start: int, n: int):
@@ -181,6 +209,7 @@ def ordered_paths(d_umem, d_desc, n: int, dev, stream, seq_sample: int = 65536) 
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import MODE_SEQUENTIAL, VM, Settings
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
     out = {"program": WORKLOADS["c2rmw"]}
     for key, mode, cnt, reps in (("lifted_parallel", 0, n, 5), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
         vm = VM(Settings(device=dev.index or 0, mode=mode))
@@ -215,6 +244,7 @@ def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536) -> 
     d_umem = torch.from_numpy(umem).to(dev)
     d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
     del umem
     out = {"program": WORKLOADS["c3learn"]}
     for key, mode, cnt, r in (("keyed", 0, n, reps), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
@@ -242,66 +272,205 @@ def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536) -> 
     return out
 
 
-def single_process_multi(args, name: str, n: int) -> None:
-    """`bench.py --gpus N` without torchrun: one process drives N GPUs through the C ABI
-    (xe_multi_create / xe_run_batch_multi: concurrent shards, RCCL delta all-reduce or in-order
-    replay), the path a Go host uses through the FFI alone. Same JSON line as the torchrun form."""
+def relaunch_ranks(gpus: int) -> int:
+    """`bench.py --gpus N` started without torchrun: the same one-process-per-GPU run the driver launches
+    (python -m torch.distributed.run ... bench.py), started as a child before anything touches the GPU,
+    so N=1..8 go through one code path (pipelined batches per rank, one shard epoch per timed region)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py")] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+# ---------------------------------------------------------------- self-verification (header-derived truth)
+def _c2_truth(idx: np.ndarray):
+    """C2 from the generated headers (no emulator involved): verdict per packet, per-proto counts."""
+    from gobpfld_amd import workloads as W
+    h = W.headers_c2(idx, 64).astype(np.int64)
+    et = (h[:, 12] << 8) | h[:, 13]
+    vlan = et == 0x8100
+    et = np.where(vlan, (h[:, 16] << 8) | h[:, 17], et)
+    l3 = np.where(vlan, 18, 14)
+    rows = np.arange(len(idx))
+    proto = np.where(et == 0x0800, h[rows, l3 + 9], np.where(et == 0x86DD, h[rows, l3 + 6], -1))
+    verdict = np.where(np.isin(proto, [1, 6, 17]), 2, 1).astype(np.uint32)
+    return verdict, np.bincount(proto[proto >= 0], minlength=256).astype(np.int64)
+
+
+def _c4_truth(idx: np.ndarray) -> np.ndarray:
+    """First match over the 48 ACL rules on the header bytes the program reads (workloads.prog_c4)."""
+    from gobpfld_amd import workloads as W
+    h = W.headers_c4(idx, 64)
+    h64 = h.astype(np.uint64)
+    ipv4 = (h[:, 12] == 0x08) & (h[:, 13] == 0x00)
+    saddr = h64[:, 26] | (h64[:, 27] << 8) | (h64[:, 28] << 16) | (h64[:, 29] << 24)
+    proto, dport = h64[:, 23], h64[:, 36] | (h64[:, 37] << 8)
+    verdict = np.full(len(h), 1, dtype=np.uint32)
+    open_ = ipv4.copy()
+    for s_le, p, dmax, action in W.acl_rules():
+        m = open_ & (saddr == np.uint64(s_le)) & (proto == np.uint64(p)) & (dport <= np.uint64(dmax))
+        verdict[m] = action
+        open_ &= ~m
+    return verdict
+
+
+def shard_truth(name: str, start: int, n: int):
+    """Expected verdicts of packets [start, start + n) and the map effect of one run over them, derived
+    from the generated headers with numpy (SURVEY §8d workloads; independent of the emulator):
+    (verdicts u32[n], delta int64 array or None). None for workloads without such a truth."""
+    from gobpfld_amd import workloads as W
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    if name == "c1":
+        return np.full(n, 2, np.uint32), None
+    if name in ("c2", "c2rmw"):  # C2-RMW: the same counters, bumped by a (lifted) load / add / store
+        return _c2_truth(idx)
+    if name == "c4":
+        return _c4_truth(idx), None
+    if name == "c3":
+        r0 = W.rng_stream(3, idx, 0)
+        hit = (W.rng_stream(3, idx, 2) % np.uint64(10)) != 0
+        fid = W.zipf_ranks((r0 >> np.uint64(11)).astype(np.float64) / float(1 << 53), W.C3_FLOWS)
+        return np.where(hit, 4, 2).astype(np.uint32), np.bincount(fid[hit], minlength=W.C3_FLOWS).astype(np.int64)
+    if name == "c5":
+        fid = W.rng_stream(5, idx, 0) % np.uint64(W.C5_FLOWS + W.C5_FLOWS // 16)
+        hit = fid < np.uint64(W.C5_FLOWS)
+        return np.full(n, 2, np.uint32), np.bincount(fid[hit].astype(np.int64), minlength=W.C5_FLOWS).astype(np.int64)
+    return None, None
+
+
+def expected_map(name: str, total: np.ndarray):
+    """The map after runs whose summed per-run effects are `total` (init + total), in xe_map_dump form."""
+    from gobpfld_amd import workloads as W
+    if name in ("c2", "c2rmw"):
+        return total.astype(np.uint64).tobytes()
+    if name in ("c3", "c5"):
+        keys, vals0 = W.c3_map_entries() if name == "c3" else W.c5_map_entries()
+        vals = vals0.view(np.uint64).reshape(-1, 2).copy()
+        if name == "c3":
+            vals[:, 1] += total.astype(np.uint64)            # {flow_id, hits}
+        else:
+            vals[:, 0] += total.astype(np.uint64)            # {pkts, bytes} of 64-byte packets
+            vals[:, 1] += total.astype(np.uint64) * np.uint64(64)
+        o = np.lexsort(keys.T[::-1])                         # xe_map_dump order: key bytes, memcmp
+        return keys[o], vals[o]
+    return None
+
+
+def verify(name: str, vm, start: int, n: int, runs: int, d_ver, dist, world: int, dev) -> dict:
+    """After the timed region: this rank's last verdicts against the truth of its shard, and its map against
+    init + runs x the sum over every rank's shard (the single VM over all shards, in order: the per-epoch
+    exchange must have made every replica exactly that). Every rank checks; `verified` is their AND."""
+    import torch
+    t0 = time.perf_counter()
+    want_v, delta = shard_truth(name, start, n)
+    if want_v is None:
+        return {"verified": None, "what": "no header-derived truth for this workload"}
+    ok_v = bool((d_ver.cpu().numpy().view(np.uint32) == want_v).all())
+    ok_m = True
+    if delta is not None:
+        t = torch.from_numpy(delta * runs).to(dev)
+        if world > 1:
+            dist.all_reduce(t)
+        exp = expected_map(name, t.cpu().numpy())
+        got = vm.map_dump(1)
+        if isinstance(exp, bytes):
+            ok_m = got == exp
+        else:
+            k, v = got
+            ok_m = (np.array_equal(np.asarray(k).reshape(exp[0].shape), exp[0]) and
+                    np.array_equal(np.frombuffer(np.asarray(v).tobytes(), np.uint64).reshape(-1, 2), exp[1]))
+    flag = torch.tensor([int(ok_v and ok_m)], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return {"verified": bool(flag.item()), "verdicts_ok_rank0": ok_v, "map_ok_rank0": ok_m if delta is not None else None,
+            "what": f"every rank: last verdicts == header truth of its shard; map == init + {runs} runs x sum over "
+                    f"{world} shard(s) of the header-derived per-run effect", "check_s": round(time.perf_counter() - t0, 2)}
+
+
+def run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream, warmup: int, steps: int, pipelined=True):
+    """Warm-up epoch, then the timed epoch: `steps` pipelined batches and (N > 1) the shard exchange (one
+    RCCL all-reduce per map, or the in-order replay), all inside the timed region. Returns the timed
+    batches' stats, elapsed max over ranks, the exchange's share of it and its outcome."""
+    import torch
+    exchanges = {"exact_sum": 0, "replayed": 0}
+
+    def sync_run():
+        return vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n, d_verdicts=d_ver.data_ptr(),
+                                   stream=stream)
+
+    def epoch_of(k: int):
+        if epoch is not None:
+            epoch.begin()
+        if pipelined:
+            hs = [vm.run_batch_device_async(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
+                                            d_verdicts=d_ver.data_ptr(), stream=stream) for _ in range(k)]
+            vm.sync()
+            sts = [h.stats() for h in hs]
+        else:
+            sts = [sync_run() for _ in range(k)]
+        t_x = time.perf_counter()
+        if epoch is not None:
+            torch.cuda.synchronize(dev)
+            t_x = time.perf_counter()
+            x = epoch.exchange([sync_run] * k)
+            exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
+        return sts, t_x
+
+    epoch_of(warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    sts, t_x = epoch_of(steps)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    t = torch.tensor([t2 - t0, t1 - t_x], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return sts, float(t[0].item()), float(t[1].item()), exchanges
+
+
+def c5_side(args, rank: int, world: int, dev, stream, dist) -> dict:
+    """BASELINE configs[4] beside the default line: 33,554,432 C5 packets per GPU (per-flow HASH counters
+    {pkts, bytes}, 1M flows), `--c5-steps` pipelined batches per rank, then the shard exchange of the
+    per-flow deltas — one RCCL all-reduce of the value region — timed separately; verified like the main
+    line (every rank's per-flow counters against the header truth summed over all shards)."""
     import torch
     from gobpfld_amd import workloads as W
-    from gobpfld_amd.emulator import Multi, VM, Settings
-    G = args.gpus
-    engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
-    vms, bufs, sizes = [], [], None
-    for k in range(G):
-        dev = torch.device("cuda", k)
-        umem, descs = W.build_batch(name, k * n, n)
-        if k == 0:
-            sizes = descs["len"].astype(np.int64)
-        bufs.append((torch.from_numpy(umem).to(dev), torch.from_numpy(descs.view(np.uint8)).to(dev),
-                     torch.zeros(n, dtype=torch.int32, device=dev)))
-        vm = VM(Settings(device=k, engine=engine))
-        W.setup_vm(vm, name)
-        vms.append(vm)
-    mu = Multi(vms)
-    args_run = ([u.data_ptr() for u, _, _ in bufs], [u.numel() for u, _, _ in bufs], [d.data_ptr() for _, d, _ in bufs],
-                [n] * G)
-    for _ in range(args.warmup):
-        mu.run(*args_run, d_verdicts=[v.data_ptr() for _, _, v in bufs])
-    for k in range(G):
-        torch.cuda.synchronize(k)
-    kernel_ms, replays, steps_retired = [], 0, 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sts, rep = mu.run(*args_run, d_verdicts=[v.data_ptr() for _, _, v in bufs])
-        kernel_ms.append(sts[0]["kernel_ms"])
-        steps_retired += sts[0]["steps"]
-        replays += int(rep)
-    for k in range(G):
-        torch.cuda.synchronize(k)
-    elapsed = time.perf_counter() - t0
-    value = n * G * args.steps / elapsed / 1e6
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
-    achieved = float(alg_bytes_per_packet(name, sizes).sum()) / avg_kernel_s / 1e9
-    traffic, traffic_src = pmc_traffic(name, n)
-    cpu = None if args.no_cpu_baseline else cpu_baseline(name, args.cpu_sample)
-    print(json.dumps({
-        "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches", "value": round(value, 3),
-        "unit": "Mpkt/s", "n_gpus": G, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic splitmix64 packets, SURVEY §8d)",
-        "config": {"workload": WORKLOADS[name], "packets_per_gpu": n, "parallelism": f"dp{G} (one process, xe_run_batch_multi)",
-                   "insns_per_packet": round(steps_retired / max(1, n * args.steps), 2), "in_order_replays": replays,
-                   "batches": "synchronous xe_run_batch_multi: every step runs the shards and reconciles the maps "
-                              "(RCCL delta all-reduce or in-order replay) — an exchange per step, unlike the "
-                              "torchrun form's one exchange per epoch of pipelined batches"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None if traffic is None else int(traffic),
-                     "traffic_source": traffic_src, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
-                     "kernel": "device 0 emulator kernel"},
-        "cpu_baseline": cpu}), flush=True)
-    mu.close()
-    for v in vms:
-        v.close()
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import ShardEpoch
+    n = args.c5_packets
+    start = rank * n
+    umem, descs = W.build_batch("c5", start, n)
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
+    del umem
+    d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    vm = VM(Settings(device=dev.index or 0))
+    W.setup_vm(vm, "c5")
+    epoch = ShardEpoch(vm, list(vm.map_defs), dist, device=dev, stream=stream) if world > 1 else None
+    sts, elapsed, x_s, exchanges = run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream,
+                                              1, args.c5_steps)
+    ver = verify("c5", vm, start, n, 1 + args.c5_steps, d_ver, dist, world, dev)
+    vbytes = vm.map_values_bytes(1)
+    vm.close()
+    kms = [st["kernel_ms"] for st in sts]
+    return {"workload": WORKLOADS["c5"], "packets_per_gpu": n, "n_gpus": world, "steps": args.c5_steps,
+            "value": round(n * world * args.c5_steps / elapsed / 1e6, 3), "unit": "Mpkt/s",
+            "ms_per_step": round(elapsed / args.c5_steps * 1e3, 4), "avg_kernel_ms": round(float(np.mean(kms)), 4),
+            "exchange_ms": round(x_s * 1e3, 4) if world > 1 else None,
+            "exchange": dict(exchanges, delta_bytes_per_gpu=vbytes, per="epoch of the timed steps") if world > 1 else None,
+            "mode": sorted({st["mode_used"] for st in sts}), **ver}
 
 
 def main() -> None:
@@ -316,19 +485,22 @@ def main() -> None:
     ap.add_argument("--engine", default="auto", choices=["auto", "interp", "jit"])
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     ap.add_argument("--no-ordered", action="store_true", help="skip the C2-RMW ordered-path lines (C2 only)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 side line (C2 only)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-run self-check")
+    ap.add_argument("--c5-packets", type=int, default=32 * 1024 * 1024, help="C5 side line: packets per GPU")
+    ap.add_argument("--c5-steps", type=int, default=8)
     ap.add_argument("--sync", action="store_true", help="one synchronous xe_run_batch_device per step (no pipelining)")
     ap.add_argument("--keyed-packets", type=int, default=4 * 1024 * 1024,
                     help="C3-learn batch of the keyed ordered-execution line (C2 runs only)")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(relaunch_ranks(args.gpus))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world == 1 and args.gpus > 1:
-        from gobpfld_amd import workloads as W
-        n1 = args.packets or (W.CONFIGS[args.config]["n"] // (8 if args.config == "c5" else 1))
-        return single_process_multi(args, args.config, n1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N-rank path on one GPU (scripts/rehearse_multi.sh): every rank on one device,
@@ -345,9 +517,7 @@ def main() -> None:
     from gobpfld_amd.shard import ShardEpoch
 
     name = args.config
-    n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))
-    if name == "c5" and not args.packets:
-        n = W.CONFIGS["c5"]["n"] // 8  # 33,554,432 per GPU
+    n = args.packets or (W.CONFIGS[name]["n"] // (8 if name == "c5" else 1))  # C5: 33,554,432 per GPU
     start = rank * n
 
     # ---- inputs resident in HBM (synthetic packets; shard = contiguous packet index range)
@@ -356,53 +526,20 @@ def main() -> None:
     d_umem = torch.from_numpy(umem).to(dev)
     d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)  # torch's stream vs the library's: the buffers are complete before any batch
 
     engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
     vm = VM(Settings(device=local, engine=engine))
     W.setup_vm(vm, name)
-    maps = list(vm.map_defs)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    exchanges = {"exact_sum": 0, "replayed": 0}
-
-    def run() -> dict:
-        return vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
-                                   d_verdicts=d_ver.data_ptr(), stream=stream)
-
     # A stream of batches through the pipelined entry point (each batch's conflict check runs on the
     # device; xe_sync completes and, if needed, replays them — all inside the timed region). N > 1:
     # the batches of a call form one shard epoch, reconciled once at its end (footprint check, one
     # RCCL all-reduce per map, or the exact in-order replay) inside the timed region.
-    pipelined = not args.sync
-    epoch = ShardEpoch(vm, maps, dist, device=dev, stream=stream) if world > 1 else None
-
-    def steps(k: int) -> list[dict]:
-        if epoch is not None:
-            epoch.begin()
-        if pipelined:
-            hs = [vm.run_batch_device_async(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), n,
-                                            d_verdicts=d_ver.data_ptr(), stream=stream) for _ in range(k)]
-            vm.sync()
-            sts = [h.stats() for h in hs]
-        else:
-            sts = [run() for _ in range(k)]
-        if epoch is not None:
-            x = epoch.exchange([run] * k)
-            exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
-        return sts
-
-    steps(args.warmup)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    epoch = ShardEpoch(vm, list(vm.map_defs), dist, device=dev, stream=stream) if world > 1 else None
+    sts, elapsed, x_s, exchanges = run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream,
+                                              args.warmup, args.steps, pipelined=not args.sync)
     kernel_ms, mode, conflicts, steps_retired, status_ok, engines, grid = [], set(), 0, 0, 0, set(), 0
-    t0 = time.perf_counter()
-    sts = steps(args.steps)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
     for st in sts:
         kernel_ms.append(st["kernel_ms"])
         mode.add(st["mode_used"])
@@ -411,10 +548,8 @@ def main() -> None:
         steps_retired += st["steps"]
         status_ok += st["status_count"][0]
         grid = st["grid_blocks"]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    # self-check outside the timed region, before anything else runs on this VM
+    check = None if args.no_verify else verify(name, vm, start, n, args.warmup + args.steps, d_ver, dist, world, dev)
 
     total_pkts = n * world * args.steps
     value = total_pkts / elapsed / 1e6
@@ -427,11 +562,14 @@ def main() -> None:
     e2e = None
     if rank == 0 and not args.no_e2e:
         e2e = e2e_baseline(vm, umem, descs)
+    del umem
+    c5 = None
+    if name == "c2" and not args.no_c5:
+        c5 = c5_side(args, rank, world, dev, stream, dist)
     ordered = None
     if rank == 0 and name == "c2" and not args.no_ordered:
         ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
         ordered["keyed_c3learn"] = keyed_paths(dev, stream, args.keyed_packets)
-    del umem
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
@@ -451,14 +589,18 @@ def main() -> None:
             "dtype": "int64",
             "data": "synthetic (deterministic splitmix64 packets, SURVEY §8d)",
             "config": {"workload": WORKLOADS[name],
-                       "packets_per_gpu": n, "packet_size": hw, "parallelism": f"dp{world} (packet shards)",
+                       "packets_per_gpu": n, "packet_size": hw,
+                       "parallelism": f"dp{world} (packet shards, one process per GPU)",
                        "insns_per_packet": round(insns_per_pkt, 2), "mode": sorted(mode),
                        "engine": sorted(engines),
                        "conflicts": conflicts, "ok_packets_per_step": status_ok // max(1, args.steps),
-                       "shard_exchanges": dict(exchanges, per="epoch of the timed steps") if world > 1 else None,
+                       "shard_exchanges": dict(exchanges, per="epoch of the timed steps",
+                                               exchange_ms=round(x_s * 1e3, 4)) if world > 1 else None,
                        "batches": "pipelined (xe_run_batch_device_async, depth 3, device-side conflict check)"
-                                  if pipelined else "synchronous (xe_run_batch_device)",
+                                  if not args.sync else "synchronous (xe_run_batch_device)",
                        "grid": grid},
+            "verified": None if check is None else check["verified"],
+            "verification": check,
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
                          "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
@@ -466,9 +608,10 @@ def main() -> None:
                          "kernel_ms_steps": [round(k, 4) for k in kernel_ms],
                          "alg_bytes_per_launch": int(bytes_per_launch),
                          "alg_bytes_per_packet": ALG_DESC.get(name, "16 desc + min(len,64) header + 4 verdict"),
-                         "issue_frac": round(insns_per_pkt * n / avg_kernel_s / ISSUE_PEAK, 5)},
+                         **sq_issue(name, n, avg_kernel_s)},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "c5": c5,
             "ordered": ordered,
         }
         print(json.dumps(out), flush=True)

@@ -40,17 +40,14 @@ def sources(cases, lib: N.Lib | None = None, variants=(0, 1, 2)) -> list[str]:
     lib = lib or host_lib()
     out = []
     for case in cases:
+        vm = VM(case[3] if not callable(case) and case[3] else Settings(), lib=lib)
         try:
             if callable(case):
-                vm = VM(Settings(), lib=lib)
                 case(vm)
             else:
-                program, maps, entries, settings = case
-                vm = VM(settings or Settings(), lib=lib)
-                idx = []
+                program, maps, entries, _ = case
                 for i, (mdef, init) in enumerate(maps):
                     m = vm.add_map(mdef, init)
-                    idx.append(m)
                     for k, v in (entries or {}).get(i, []):
                         if k is None:
                             vm.map_push(m, v)
@@ -58,13 +55,11 @@ def sources(cases, lib: N.Lib | None = None, variants=(0, 1, 2)) -> list[str]:
                             vm.map_update(m, k, v)
                 progs = program if program and isinstance(program[0], list) else [program]
                 vm.set_entrypoint([vm.add_raw_program(x) for x in progs][0])
-        except EmulatorError:
-            continue
-        try:
             out += vm.kernel_sources(variants)
         except EmulatorError:
-            pass
-        vm.close()
+            continue  # a case the emulator refuses (it is tested for that) has no kernel
+        finally:
+            vm.close()
     return list(dict.fromkeys(out))
 
 

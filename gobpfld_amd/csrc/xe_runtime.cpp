@@ -876,7 +876,11 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc, bool hash) {
   if (const char* e = xe_tuning_env("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));
   uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
-  while (want > 1 && uint64_t(want) * (hash ? live : vals_alloc) > (160ull << 20)) want >>= 1;
+  // the fold reads the live bytes of every replica; the replicas themselves span the whole region (a
+  // sparse HASH table's too), so their memory is bounded separately (C3: 16 x 32 MB)
+  while (want > 1 && (uint64_t(want) * (hash ? live : vals_alloc) > (160ull << 20) ||
+                      uint64_t(want) * vals_alloc > (1ull << 30)))
+    want >>= 1;
   return want;
 }
 
@@ -1166,16 +1170,26 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       if (map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
     }
     const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
-    const uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc, m.dkind == XE_DM_HASH) : 1u;
+    uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc, m.dkind == XE_DM_HASH) : 1u;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
       dev_free(m.d_rep);
       m.d_rep = nullptr;
+      const uint32_t had = m.nrep;
       m.nrep = 1;
-      if (want > 1 && (dev_alloc((void**)&m.d_rep, m.rep_stride * want) ||
-                       dmemset(m.d_rep, 0, m.rep_stride * want, vm->stream) || dsync(vm->stream)))
-        return fail(vm, XE_ERR_DEVICE, "device alloc (map replicas)");
+      // replicas only spread contended adds: when the device cannot hold them, run without
+      while (want > 1 && dev_alloc((void**)&m.d_rep, m.rep_stride * want)) {
+        m.d_rep = nullptr;
+        want >>= 1;
+      }
+      if (want > 1 && (dmemset(m.d_rep, 0, m.rep_stride * want, vm->stream) || dsync(vm->stream)))
+        return fail(vm, XE_ERR_DEVICE, "device memset (map replicas)");
+      if (want <= 1) {
+        dev_free(m.d_rep);
+        m.d_rep = nullptr;
+        want = 1;
+      }
       m.nrep = want;
-      vm->jit_idx = -1;  // the replica count is compiled into the per-program kernel
+      if (m.nrep != had) vm->jit_idx = -1;  // the replica count is compiled into the per-program kernel
     }
     if (xe_tuning_env("XE_PRINT_ALLOC"))  // placement experiments (tuning build only)
       fprintf(stderr, "{\"map\": %zu, \"vals\": \"%p\", \"keys\": \"%p\", \"rep\": \"%p\", \"nrep\": %u, \"rep_stride\": %llu}\n",

@@ -27,10 +27,14 @@ def _bufs(vm, maps, device, attr, size_of):
     if cache is None:
         cache = {}
         setattr(vm, attr, cache)
+    grew = False
     for m in maps:
         need = size_of(m)
         if m not in cache or cache[m].numel() < need:
             cache[m] = torch.zeros(need, dtype=torch.uint8, device=device)
+            grew = True
+    if grew:
+        _collective_done(device)  # the zero fill (torch's stream) lands before the library writes
     return cache
 
 
@@ -41,8 +45,18 @@ def _gather_check(vm, dist, device):
     t = torch.from_numpy(fp.view(np.int64).copy()).to(device)
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
-    fps = np.concatenate([p.cpu().numpy() for p in parts]).view(np.uint64)
+    fps = np.concatenate([p.cpu().numpy() for p in parts]).view(np.uint64)  # .cpu() waits for the gather
     return vm.shard_check(fps, world)
+
+
+def _collective_done(device) -> None:
+    """The library's launches run on the stream it is given — or, for stream 0, on the VM's own stream,
+    which is not torch's default stream (whose handle is also 0). A collective's result is only ordered
+    before work on torch's current stream, so the host waits for it before the library reads it."""
+    import torch
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
 
 
 def _sum_deltas(vm, maps, dist, lanes, device, stream) -> None:
@@ -62,6 +76,7 @@ def _sum_deltas(vm, maps, dist, lanes, device, stream) -> None:
             dist.all_reduce(buf[: vbytes[m]])
         else:  # 4, and 2 (u32 containers, twice the region)
             dist.all_reduce(buf[: vbytes[m] * (2 if lane == 2 else 1)].view(torch.int32))
+        _collective_done(device)
         vm.map_apply_delta(m, buf.data_ptr(), stream=stream, lane=lane)
 
 
@@ -75,11 +90,12 @@ def _mover(vm, maps, dist, device, stream):
         for m in maps:
             size = torch.tensor([vm.map_state_bytes(m) if rank == src else 0], dtype=torch.int64, device=device)
             dist.broadcast(size, src=src)
-            nb = int(size.item())
+            nb = int(size.item())  # (.item() waits for the broadcast)
             b = _bufs(vm, [m], device, "_shard_state_bufs", lambda _m: nb)[m][:nb]
             if rank == src:
                 vm.map_state_export(m, b.data_ptr(), stream=stream)
             dist.broadcast(b, src=src)
+            _collective_done(device)
             if import_on(rank) and rank != src:
                 vm.map_state_import(m, b.data_ptr(), stream=stream)
     return move

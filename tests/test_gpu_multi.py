@@ -141,3 +141,62 @@ def test_shard_epoch_bench_path_one_rank(gpu_lib, oracle_lib):
         vm.close()
     finally:
         dist.destroy_process_group()
+
+
+def _gloo_rank(rank, world, port, name, n, k, out):
+    """One rank of the bench's N > 1 path (ShardEpoch over torch.distributed) sharing cuda:0 with the
+    other over gloo: pipelined batches, the exchange, then the map against the header truth."""
+    import importlib.util
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import ShardEpoch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    vm = VM(Settings())
+    W.setup_vm(vm, name)
+    umem, descs = W.build_batch(name, rank * n, n)
+    du, dd = torch.from_numpy(umem).to(dev), torch.from_numpy(descs.view(np.uint8)).to(dev)
+    ver = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev).cuda_stream  # 0 on the default stream: the library uses its own
+    ep = ShardEpoch(vm, list(vm.map_defs), dist, device=dev, stream=stream)
+    run = lambda: vm.run_batch_device(du.data_ptr(), du.numel(), dd.data_ptr(), n, d_verdicts=ver.data_ptr(), stream=stream)
+    exact = []
+    for _ in range(2):  # two epochs of k pipelined batches
+        ep.begin()
+        for _ in range(k):
+            vm.run_batch_device_async(du.data_ptr(), du.numel(), dd.data_ptr(), n, d_verdicts=ver.data_ptr(), stream=stream)
+        vm.sync()
+        exact.append(ep.exchange([run] * k)["exact_sum"])
+    r = B.verify(name, vm, rank * n, n, 2 * k, ver, dist, world, dev)
+    np.save(os.path.join(out, f"r{rank}.npy"), np.array([r["verified"], r["map_ok_rank0"], all(exact)]))
+    vm.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["c5", "c3", "c2"])
+def test_shard_epoch_two_ranks_share_one_gpu(tmp_path, name):
+    """bench.py's N > 1 exchange with two processes on cuda:0 (gloo): after two epochs every rank's map
+    is init + 4 runs x (shard 0 + shard 1) of the header truth. Catches the library reading a delta
+    buffer before the collective that fills it has landed (stream 0 is not torch's default stream)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_gloo_rank, args=(2, port, name, 1 << 18, 2, str(tmp_path)), nprocs=2)
+    for r in range(2):
+        verified, map_ok, exact = np.load(tmp_path / f"r{r}.npy", allow_pickle=False)
+        assert exact and map_ok and verified, f"{name}: rank {r}: exact {exact} map {map_ok} verified {verified}"

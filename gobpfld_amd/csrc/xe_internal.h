@@ -238,7 +238,8 @@ XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
 #define XE_KINS 2u            // ikey slots per packet (more held-back inserts: the one-lane replay)
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
 enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
-                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW, XE_KS_CFLAG, XE_KS_CLIST };
+                  XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW, XE_KS_CFLAG, XE_KS_CLIST,
+                  XE_KS_LRUID };
 // Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
 // a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
 // a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
@@ -253,7 +254,7 @@ enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_
 #define XE_KS_CNEXT 69                      // the chain pass's work queue: next unclaimed chain
 #define XE_KS_CINS 128                      // [64 maps][XE_KSTRIPES] inserts the chains made
 #define XE_KS_WORDS (128 + 64 * XE_KSTRIPES)
-#define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid
+#define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid | LRU value id << 32
 #define XE_KID_ARRAY_TAG 0xA7A7A7A700000000ull
 #define XE_KID_NIL_KEY 0x6e696c6b65790001ull  // the nil (empty) hash key
 

@@ -986,7 +986,13 @@ XE_DEV int key_touch_mem(XeLane& L, const XeParams& P, uint32_t h, const XeBMem&
   if (!B.map || (P.mode != XE_MODE_SPEC && P.mode != XE_MODE_CHAIN)) return 0;
   const XeDevMap M = map_desc(L, B.map);
   if (B.array) return key_touch_array(L, P, B.map, M, off, size, write, dkey);
-  if (M.kind != XE_DM_HASH) return 0;  // the ordered maps never run keyed
+  if (M.kind == XE_DM_LRU && xe_h_cls(h) == XE_H_HASH) {  // an LRU value: the key of its slot record
+    if (h == L.kh) return key_touch(L, P, L.kk, write, dkey);
+    const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(xe_h_slot(h)) + 2];
+    return key_touch(L, P, kid_slot(B.map, M, slot), write, dkey);
+  }
+  // queue / stack elements and perf events follow packet order: a write to one is never keyed
+  if (M.kind != XE_DM_HASH) return write ? XE_EV_ORD : 0;
   return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, xe_h_slot(h)), write, dkey);
 }
 #endif
@@ -1612,7 +1618,7 @@ XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty, uns
       bool eq = true;
       for (uint32_t k = 0; k < M.kwords; k++) eq = eq && r[1 + k] == kw[k];
       if (eq) {
-        r[0] = XE_SLOT_FULL;
+        r[0] = (r[0] & ~0xffffffffull) | XE_SLOT_FULL;  // an LRU record keeps its reserved value id
         xe_wave_count(cnt, true);
         return int64_t(idx);
       }
@@ -1627,7 +1633,9 @@ XE_DEV int64_t hash_claim(const XeDevMap& M, const uint64_t* kw, bool empty, uns
 // then the key words, then the tombstone state marked NEW. Records claimed in this launch (BUSY, NEW)
 // hold other keys (each key has one reserving lane) and are passed without reading their key words,
 // so no load needs acquire ordering. Returns false when the table has no free slot.
-XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw) {
+// hi: the record's high word for an LRU map (its reserved value id << 32), 0 for HASH; a tombstone already
+// holding the key (an earlier unused reservation, an LRU eviction) takes it too.
+XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw, uint64_t hi = 0) {
   const uint32_t mask = M.cap - 1;
   uint32_t idx = uint32_t(xe_hash_words(kw, M.kwords, M.key_size)) & mask;
 #pragma unroll 1
@@ -1638,11 +1646,14 @@ XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw) {
     if ((st & (XE_SLOT_FULL | XE_SLOT_TOMB)) && !(st & XE_SLOT_NEW)) {
       bool eq = true;
       for (uint32_t k = 0; k < M.kwords; k++) eq = eq && ((XE_GP(const uint64_t))r)[1 + k] == kw[k];
-      if (eq) return true;
+      if (eq) {
+        if (hi && !(st & XE_SLOT_FULL)) ((XE_GP(uint64_t))r)[0] = XE_SLOT_TOMB | hi;
+        return true;
+      }
     } else if (!(st & (XE_SLOT_BUSY | XE_SLOT_NEW | XE_SLOT_FULL | XE_SLOT_TOMB))) {
       if (xe_atomic_cas64(r, w0, XE_SLOT_BUSY) != w0) continue;  // lost the slot: look at it again
       for (uint32_t k = 0; k < M.kwords; k++) ((XE_GP(uint64_t))r)[1 + k] = kw[k];
-      ((XE_GP(uint64_t))r)[0] = XE_SLOT_TOMB | XE_SLOT_NEW;
+      ((XE_GP(uint64_t))r)[0] = XE_SLOT_TOMB | XE_SLOT_NEW | hi;
       return true;
     }
     idx = (idx + 1) & mask;
@@ -1699,6 +1710,13 @@ XE_DEV void lru_promote(const XeDevMap& M, uint32_t v) {  // promote, :51-68
   lru_push_front(M, v);
 }
 XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_word0(M, uint64_t(slot)) >> 32); }
+// Concurrent modes: a touch (lookup hit, update) of value v by this packet — its last touch in packet order
+// is what the UsageList keeps (the runtime relinks by it, lru_finalize)
+XE_DEV int lru_touch(XeLane& L, const XeDevMap& M, uint32_t v) {
+  if (L.oseq >= 0xffffu) return XE_EV_ORD;
+  xe_atomic_max64((unsigned long long*)M.tag + v, ((uint64_t(L.pidx) << 16) | L.oseq++) + 1);
+  return 0;
+}
 // LRU lookup of a key (no promotion); value id or XE_NONE
 XE_DEV uint32_t lru_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
   const int64_t s = hash_find(M, kw, empty);
@@ -1790,8 +1808,8 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
     if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2)) return e;
 #if XE_KEYED
     uint64_t kid = 0;
-    if (M.kind == XE_DM_HASH && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)) {  // the key's presence is read
-      kid = kid_hash(m, M, kw, empty);
+    if ((M.kind == XE_DM_HASH || M.kind == XE_DM_LRU) && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)) {
+      kid = kid_hash(m, M, kw, empty);  // the key's presence is read
       if (int e = key_touch(L, P, kid, false)) return e;
     }
 #endif
@@ -1799,13 +1817,15 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
     if (M.kind == XE_DM_LRU) {
       const uint32_t v = lru_find(M, kw, empty);
       if (v == XE_NONE) return 0;
-      if (P.mode == XE_MODE_PARALLEL) {
+      if (xe_concurrent(P)) {
         // a lookup promotes (maps_hash_lru.go:70-91): in packet order the key ends up at the head as
         // often as it was touched last; the run keeps each value's last touch (packet << 16 | call) + 1
         // and the runtime moves the touched keys to the UsageList's head by it (ordered_finalize)
-        if (L.oseq >= 0xffffu) return XE_EV_ORD;
-        xe_atomic_max64((unsigned long long*)M.tag + v, ((uint64_t(L.pidx) << 16) | L.oseq++) + 1);
+        if (int e = lru_touch(L, M, v)) return e;
         out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
+#if XE_KEYED
+        if (kid) { L.kh = out.h; L.kk = kid; }
+#endif
         return 0;
       }
       lru_promote(M, v);
@@ -1822,7 +1842,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
   }
 #if XE_HAS_ORDERED
   if (M.kind == XE_DM_LIST || M.kind == XE_DM_PERF) {
-    if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;  // the list changes in packet order
+    if (xe_concurrent(P)) return XE_EV_ORD;  // the list changes in packet order
     int64_t kv = 0;
     if (!peek) {
       int64_t off = XE_T_KIND(K.t) == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, K.v) : K.v;
@@ -1966,8 +1986,16 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
     if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
+#if XE_KEYED
+    const uint64_t kid = kid_hash(m, M, kw, empty);
+    if (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)
+      if (int e = key_touch(L, P, kid, false)) return e;  // presence (and the count) are read
+#endif
     uint32_t v = lru_find(M, kw, empty);
     if (v == XE_NONE && *map_hdr(M, 2) + 1 > M.max_entries) {
+      // an eviction depends on the whole batch's order of touches: the keyed schedule only runs when
+      // count + the batch's written keys fit MaxEntries (xe_runtime.cpp keyed), else the in-order replay
+      if (xe_concurrent(P)) return XE_EV_ORD;
       const uint32_t tail = uint32_t(*map_hdr(M, 1));
       if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
       if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, tail))) return e;
@@ -1976,8 +2004,40 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
     int ve = ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
     if (XE_IS_PANIC(ve)) return ve;
+#if XE_KEYED
+    if (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)
+      if (int e = key_touch(L, P, kid, true)) return e;
+    if (P.mode == XE_MODE_SPEC) {  // held back; a new key goes to the insert log (its record is reserved)
+      if (v == XE_NONE) {
+        if (L.kins >= XE_KINS) {
+          L.kn = XE_KLOG + 1;  // more inserts than slots: reported as a key-log overflow
+        } else {
+          XE_GP(uint64_t) en = (XE_GP(uint64_t))P.K.ikey + (uint64_t(L.kpkt) * XE_KINS + L.kins) * P.K.kw;
+#pragma unroll
+          for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++)
+            if (w + 1 < P.K.kw) en[1 + w] = kw[w];
+          en[0] = uint64_t(m) | (empty ? 0x100ull : 0ull) | XE_KEY_VALID;
+#pragma unroll
+          for (uint32_t j = 0; j < XE_KLOG; j++)
+            if (j < L.kn && (L.klog[j] & ~XE_KLOG_FLAGS) == kid) L.klog[j] |= XE_KLOG_INS | (uint64_t(L.kins) << 3);
+          L.kins++;
+        }
+      }
+      return helper_errno_result(L, 0);
+    }
+    if (P.mode == XE_MODE_CHAIN && v == XE_NONE) {
+      // the record reserved for this key holds its value id (xe_runtime.cpp keyed: XE_KS_LRUID, RESERVE)
+      const int64_t slot = empty ? -1 : hash_claim(M, kw, false, P.K.cins + m * XE_KSTRIPES + (L.wave % XE_KSTRIPES));
+      if (slot < 0) return XE_EV_ORD;  // the nil key (no reservation) or a key that left its chain
+      v = lru_vid(M, slot);
+      *lru_link(M, v, 2) = uint32_t(slot);
+    }
+#endif
     if (v == XE_NONE) {
       if (int e = lru_insert(M, kw, empty, v)) return e;
+    } else if (xe_concurrent(P)) {
+      if (int e = lru_touch(L, M, v)) return e;  // appended + promoted, or promoted (:144-150)
+      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
     } else {
       lru_promote(M, v);
       if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
@@ -2109,7 +2169,7 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       const XeReg R5 = reg_get(L, 5);
       XE_NILCHK(R5);
       int64_t err;
-      if (P.mode == XE_MODE_PARALLEL) {  // appended in packet order after the run (list_push_par)
+      if (xe_concurrent(P)) {  // appended in packet order after the run (list_push_par)
         if (int e = list_push_par(L, P, m, M, reg_get(L, 4), R5.v, err)) return in_helper(e);
         return helper_errno_result(L, err);
       }
@@ -2123,7 +2183,7 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       const XeDevMap M = map_desc(L, m);
       if (M.kind != XE_DM_LIST && M.kind != XE_DM_PERF) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "push not available"
       int64_t err;
-      if (P.mode == XE_MODE_PARALLEL) {
+      if (xe_concurrent(P)) {
         if (int e = list_push_par(L, P, m, M, reg_get(L, 2), int64_t(M.value_size), err)) return in_helper(e);
         return helper_errno_result(L, err);
       }
@@ -2137,7 +2197,7 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
       const XeDevMap M = map_desc(L, m);
       if (M.kind != XE_DM_LIST) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "pop not available"
-      if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
+      if (xe_concurrent(P)) return XE_EV_ORD;
       XeReg val{0, 0, XE_KIND_IMM};
       const uint64_t cnt = *map_hdr(M, 1);
       if (cnt) {
@@ -2989,7 +3049,23 @@ XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t 
   uint64_t kw[XE_MAX_KEY / 8];
 #pragma unroll
   for (uint32_t w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = w + 1 < K.kw ? en[1 + w] : 0;
-  if (!hash_reserve(maps[m], kw)) xe_atomic_or32(K.err, 2u);
+  // an LRU key's record carries the value id XE_KS_LRUID gave it
+  const uint64_t hi = maps[m].kind == XE_DM_LRU ? (en[0] & ~0xffffffffull) : 0ull;
+  if (!hash_reserve(maps[m], kw, hi)) xe_atomic_or32(K.err, 2u);
+}
+// D slot x: a new LRU key gets a value id from its map's pool (next id, hdr[3]); lanes taking ids from
+// the same map share one atomic per wave. Every lane of the launch calls this (no early exit).
+XE_DEV void keyed_lruid_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x) {
+  bool want = false;
+  uint32_t m = 0;
+  XE_GP(uint64_t) en = (XE_GP(uint64_t))K.dkey + uint64_t(x) * K.kw;
+  if (((XE_GP(const unsigned long long))K.dkid)[x] && (en[0] & XE_KEY_VALID) && !(en[0] & 0x100ull)) {
+    m = uint32_t(en[0] & 0xffu);
+    want = maps[m].kind == XE_DM_LRU;
+  }
+  unsigned int* next = want ? (unsigned int*)maps[m].hdr + 6 : (unsigned int*)K.err;  // hdr[3], low word
+  const uint32_t id = xe_wave_alloc_at(next, want);
+  if (want) en[0] = (en[0] & 0xffffffffull) | (uint64_t(id) << 32);
 }
 // D slot x, after the chains: the reservation of a new HASH key loses its "claimed in this launch" mark
 // (a chain's insert already turned it FULL; an unused one stays a plain tombstone holding its key), so a
@@ -3049,6 +3125,7 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_UNNEW: keyed_unnew_item(K, maps, i); break;
     case XE_KS_CFLAG: keyed_cflag_item(K, i); break;
     case XE_KS_CLIST: keyed_clist_item(K, i); break;
+    case XE_KS_LRUID: keyed_lruid_item(K, maps, i); break;
     default: break;
   }
 }
@@ -3098,6 +3175,10 @@ XE_DEV void chain_packets(XeLane& L, const XeParams& P, uint32_t g, uint32_t nth
     L.kchain = key;
     lane_reset(L, P, i, have);
     key_begin(L, i);
+#if XE_HAS_ORDERED
+    L.pidx = i;  // order keys of the packet's appends and LRU touches
+    L.oseq = 0;
+#endif
     body(i, have);
     if (have && ++p >= pend) have = false;
   }

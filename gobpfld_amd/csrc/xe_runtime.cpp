@@ -797,7 +797,7 @@ static void keyed_free(xe_vm* vm) {
 static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
   uint32_t kw = 1;  // dkey entry: map word + the longest HASH key
   for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].dkind == XE_DM_HASH) kw = std::max(kw, 1 + vm->maps[i].kwords);
+    if (vm->maps[i].dkind == XE_DM_HASH || vm->maps[i].dkind == XE_DM_LRU) kw = std::max(kw, 1 + vm->maps[i].kwords);
   XeKeyed& K = vm->kd;
   if (vm->keyed_n < n || !vm->d_ksmall || vm->keyed_kw < kw) {
     dev_free(K.klog); dev_free(K.kcnt); dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.iota);
@@ -1273,9 +1273,14 @@ XeGen gen_layout(uint32_t nl, uint32_t nobj, uint32_t nframes, uint32_t nvc, uin
 // chunks, see parallel_packets), never more than one 64-packet chunk per wave. A second generation of
 // blocks would run its full share after the first finishes, and every extra wave adds its per-wave
 // flush (map atomics, statistics) to the same few addresses.
+// At most 4 blocks (16 waves) per CU even when more would be resident: C2 0.300 -> 0.279 ms at 16 waves
+// against 24 (6 blocks), the same floor the bare access pattern shows (tools/sol_c2.hip: 16 waves
+// per CU fastest); C3-C5 were already at 16 and lose below it (profiles/r4/grid_ab.json).
+constexpr int kMaxBlocksPerCu = 4;
 uint32_t grid_blocks(uint32_t n, int per_cu, int cus) {
   uint64_t chunks = (uint64_t(n) + 63) / 64;
   uint64_t blocks = (chunks + 3) / 4;  // 4 waves per 256-thread block
+  if (per_cu > kMaxBlocksPerCu) per_cu = kMaxBlocksPerCu;
   uint64_t maxb = (per_cu > 0 && cus > 0) ? uint64_t(per_cu) * uint64_t(cus) : 256ull * 4;
   if (const char* e = xe_tuning_env("XE_MAX_BLOCKS")) maxb = std::max(1ll, atoll(e));
   return uint32_t(std::max<uint64_t>(1, std::min(blocks, maxb)));
@@ -1715,15 +1720,22 @@ static bool has_callbpf(const xe_vm* vm) {
 // packet order after the run) and LRU_HASH lookups (promotions, applied by last touch after the run);
 // any other operation on them (pops, peeks, list / event lookups, LRU updates and deletes) raises
 // XE_FLAG_ORDERED and the batch replays in packet order.
-static bool ordered_parallel_ok(const xe_vm*) { return true; }
+static bool ordered_parallel_ok(const xe_vm* vm) {
+  // a static screen: pops and peeks (helpers 88 / 89) take the list's head in packet order, so a VM whose
+  // programs can call them skips the parallel try (and its rollback) and replays in order straight away
+  for (size_t p = 1; p < vm->programs.size(); p++)
+    for (const XeUop& u : vm->programs[p])
+      if (u.cls == U_HELPER && (u.imm == 88 || u.imm == 89)) return false;
+  return true;
+}
 // the ordered maps' header words (counts, next ids, event bytes) at the start of a parallel run, and
 // the LRU maps' value pools (a parallel run adds into looked-up values in place)
-static int ordered_hdr_read(xe_vm* vm, std::vector<uint64_t>& out, xe_stream_t s) {
+static int ordered_hdr_read(xe_vm* vm, std::vector<uint64_t>& out, xe_stream_t s, bool snap_pools = true) {
   out.assign(vm->maps.size() * 8, 0);
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.ordered() && d2h(&out[i * 8], m.d_hdr, 64, s)) return -1;
-    if (m.dkind == XE_DM_LRU) {
+    if (snap_pools && m.dkind == XE_DM_LRU) {
       const uint64_t vb = uint64_t(m.pool_cap) * m.def.value_size;
       if (ensure_dev(&m.d_vsnap, m.n_vsnap, vb) || (vb && d2d(m.d_vsnap, m.d_vals, vb, s))) return -1;
     }
@@ -1777,7 +1789,7 @@ static int lru_finalize(xe_vm* vm, HostMap& m, xe_stream_t s) {
 // put the appends of a parallel run (header words `h0` before it) into packet order
 static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t n, xe_stream_t s) {
   std::vector<uint64_t> h1;
-  if (ordered_hdr_read(vm, h1, s)) return -1;
+  if (ordered_hdr_read(vm, h1, s, false)) return -1;  // the header words only (no pool snapshot)
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.dkind == XE_DM_LRU) {
@@ -2198,6 +2210,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     }
     return 0;
   };
+  const bool ordmaps = has_ordered_maps(vm);
   // Keyed ordered execution (xe_internal.h): the SPEC pass, the build, the parallel pass of the packets
   // on no chain, the chains. Returns 1 when the batch has to take the one-lane replay instead (maps,
   // packets and records rolled back), 0 when done (used: XE_MODE_PARALLEL when no packet wrote a map
@@ -2212,6 +2225,19 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     const uint64_t dwant = vm->keyed_dnext ? vm->keyed_dnext : std::max<uint64_t>(4096, n / 4);
     while (dcap < dwant && dcap < dmax) dcap <<= 1;
     if (keyed_alloc(vm, n, dcap)) return fail(vm, XE_ERR_NOMEM, "device alloc (keyed execution)");
+    // ordered maps (LRU_HASH keys, appends): the host mirror holds the batch's start (rollback(true)
+    // rebuilds the device copies from it), kh0 their header words / LRU value pools for the cheaper
+    // rollbacks before any record was claimed
+    std::vector<uint64_t> kh0;
+    if (ordmaps) {
+      for (size_t i = 1; i < vm->maps.size(); i++)
+        if (vm->maps[i].ordered() && map_download(vm, vm->maps[i])) return fail(vm, XE_ERR_DEVICE, "map download");
+      if (ordered_hdr_read(vm, kh0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
+    }
+    auto krollback = [&]() -> int {
+      if (rollback(false)) return -1;
+      return ordmaps ? ordered_hdr_restore(vm, kh0, s) : 0;
+    };
     XeKeyed K = vm->kd;
     K.n = n;
     if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, XE_KS_WORDS * 4, s))
@@ -2225,9 +2251,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (klaunch(&X, grid) || fold()) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed spec)");
     if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed spec)");
     uint32_t flags = uint32_t(red[0]);
-    if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) return rollback(false) ? -1 : 1;
+    if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) return krollback() ? -1 : 1;
     if (!(flags & XE_FLAG_KEYED)) {  // no packet wrote a map entry: an ordinary parallel run
-      if (run_conflict(red, P.nmaps)) return rollback(false) ? -1 : 1;
+      if (run_conflict(red, P.nmaps)) return krollback() ? -1 : 1;
+      if (ordmaps && ordered_finalize(vm, kh0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
       used_out = XE_MODE_PARALLEL;
       return 0;
     }
@@ -2237,7 +2264,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     auto read_small = [&]() { return d2h(small.data(), vm->d_ksmall, XE_KS_WORDS * 4, s) || dsync(s); };
     if (step(XE_KS_DSET, n)) return fail(vm, XE_ERR_DEVICE, "keyed build");
     for (int round = 0;; round++) {
-      if (round >= 64) return rollback(false) ? -1 : 1;
+      if (round >= 64) return krollback() ? -1 : 1;
       if (dmemset(K.changed, 0, 4, s) || step(XE_KS_UNION, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
       if (!small[XE_KS_CHANGED]) break;
     }
@@ -2245,9 +2272,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       return fail(vm, XE_ERR_DEVICE, "keyed build");
     if (small[XE_KS_ERR] & 8u) {  // D outgrew its table: once more with room for every packet's key
       vm->keyed_dnext = dmax;
-      if (dcap < dmax) return rollback(false) ? -1 : 2;
+      if (dcap < dmax) return krollback() ? -1 : 2;
     }
-    if (small[XE_KS_ERR]) return rollback(false) ? -1 : 1;  // key log overflow
+    if (small[XE_KS_ERR]) return krollback() ? -1 : 1;  // key log overflow
     {
       uint64_t nd = 0;
       for (uint32_t i = 0; i < 64; i++) nd += small[XE_KS_DCOUNT + i];
@@ -2255,14 +2282,29 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       while (next < 4 * nd && next < dmax) next <<= 1;
       vm->keyed_dnext = uint32_t(next);
     }
-    // a HASH insert can fail for capacity only in an order-dependent way: every key of D fits
+    // a HASH insert can fail for capacity only in an order-dependent way (and an LRU insert would evict
+    // by the batch's order of touches): every key of D fits
     for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];
       const uint64_t nd = small[XE_KS_DCOUNT + i];
-      if (m.dkind != XE_DM_HASH || !nd) continue;
-      uint32_t cnt = 0;
-      if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
-      if (uint64_t(cnt) + nd > m.def.max_entries) return rollback(false) ? -1 : 1;
+      if ((m.dkind != XE_DM_HASH && m.dkind != XE_DM_LRU) || !nd) continue;
+      uint64_t cnt = 0;
+      if (m.dkind == XE_DM_HASH) {
+        uint32_t c32 = 0;
+        if (d2h(&c32, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+        cnt = c32;
+      } else {
+        cnt = kh0[i * 8 + 2];
+        if (kh0[i * 8 + 3] + nd > m.pool_cap) {  // value ids for every new key: grow the pool, run again
+          if (krollback()) return -1;
+          vm->ord_slack = std::max<uint64_t>(vm->ord_slack, 2 * nd + 4096);
+          m.host_dirty = true;  // the mirror is the batch's start: rebuilt with the larger pool
+          if (prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "ordered map room");
+          P.maps = vm->d_maps;
+          return 2;
+        }
+      }
+      if (cnt + nd > m.def.max_entries) return krollback() ? -1 : 1;
     }
     uint32_t end_bit = 1;
     while ((1ull << end_bit) <= K.dcap) end_bit++;
@@ -2275,9 +2317,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     // one chain with more than half the packets (a hot key written by most of them): its lane would
     // take longer than the staged one-lane replay of the whole batch
     if (step(XE_KS_CSTART, K.nO) || step(XE_KS_CLONG, K.nO) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
-    if (small[XE_KS_LONG]) return rollback(false) ? -1 : 1;
+    if (small[XE_KS_LONG]) return krollback() ? -1 : 1;
     // 3. back to the start state; reserve a slot record for every new HASH key of D
-    if (rollback(false) || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
+    if (krollback() || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
+    if (ordmaps && step(XE_KS_LRUID, K.dcap)) return fail(vm, XE_ERR_DEVICE, "keyed value ids");
     if (step(XE_KS_RESERVE, K.dcap) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");
     if (small[XE_KS_ERR]) return rollback(true) ? -1 : 1;
     // 4. the packets on no chain, in parallel (the fast kernel: the skip mask is its only keyed input)
@@ -2305,17 +2348,26 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (klaunch(&X, cgrid) || step(XE_KS_UNNEW, K.dcap)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
     if (read_aux() || read_small()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
     if (run_conflict(red, P.nmaps)) return rollback(true) ? -1 : 1;  // a packet left its chain / an order-dependent add
-    // the chains' inserts into the map counts
+    // the chains' inserts into the map counts (LRU_HASH: header word 2)
     for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];
       uint32_t add = 0;
       for (uint32_t k = 0; k < XE_KSTRIPES; k++) add += small[XE_KS_CINS + i * XE_KSTRIPES + k];
-      if (m.dkind != XE_DM_HASH || !add) continue;
-      uint32_t cnt = 0;
-      if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
-      cnt += add;
-      if (h2d(m.d_count, &cnt, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+      if (!add) continue;
+      if (m.dkind == XE_DM_HASH) {
+        uint32_t cnt = 0;
+        if (d2h(&cnt, m.d_count, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+        cnt += add;
+        if (h2d(m.d_count, &cnt, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+      } else if (m.dkind == XE_DM_LRU) {
+        uint64_t cnt = 0;
+        if (d2h(&cnt, m.d_hdr + 2, 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+        cnt += add;
+        if (h2d(m.d_hdr + 2, &cnt, 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
+      }
     }
+    // the appends and LRU touches of both passes into packet order
+    if (ordmaps && ordered_finalize(vm, kh0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
     vm->last_grid = grid;
     used_out = XE_MODE_KEYED;
     return 0;
@@ -2326,11 +2378,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   bool conflict = false;
   uint32_t used = XE_MODE_PARALLEL;
   float kms = 0;
-  const bool ordmaps = has_ordered_maps(vm);
-  const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && !ordmaps;
-  // ordered maps: appends run in parallel (put in packet order afterwards); a batch with any other
-  // operation on them replays in order, and so do the next few after such a batch
-  bool ord_seq = mode == XE_MODE_AUTO && ordmaps && (!ordered_parallel_ok(vm) || vm->ord_backoff);
+  // ordered maps: appends and LRU lookups run in parallel (put in packet order afterwards), LRU updates
+  // through the keyed path; a batch with any other operation on them (pops, peeks, list lookups, an LRU
+  // eviction) replays in order, and so do the next few after such a batch
+  const bool ord_par = !ordmaps || ordered_parallel_ok(vm);
+  const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && ord_par;
+  bool ord_seq = mode == XE_MODE_AUTO && ordmaps && (!ord_par || vm->ord_backoff);
   if (ord_seq && vm->ord_backoff) vm->ord_backoff--;
   std::vector<uint64_t> ord_h0;
   if (mode == XE_MODE_SEQUENTIAL || ord_seq || overlap) {
@@ -2339,10 +2392,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   } else if (keyed_ok && vm->keyed_hint) {
     // the last batch wrote map entries: straight to the keyed path
     int r = keyed(used);
-    if (r == 2) r = keyed(used);  // its D table was too small
+    for (int t = 0; r == 2 && t < 3; t++) r = keyed(used);  // its D table / an LRU pool was too small
+    if (r == 2) r = 1;
     if (r < 0) return r;
     if (r == 1) {
       vm->keyed_backoff = kKeyedBackoff;
+      if (ordmaps) vm->ord_backoff = kKeyedBackoff;
       used = XE_MODE_SEQUENTIAL;
       if (int rc = sequential(kms)) return rc;
     }
@@ -2383,17 +2438,16 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the
       // keyed path, everything else (and what the keyed path refuses) the replay in packet order
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
-      if (ordmaps) {  // the appends of the run are past the restored counts: unreferenced
+      if (ordmaps)  // the appends of the run are past the restored counts: unreferenced
         if (ordered_hdr_restore(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "rollback (ordered maps)");
-        vm->ord_backoff = kKeyedBackoff;
-      }
       int r = 1;
       const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY);
       if (try_keyed && vm->keyed_backoff) vm->keyed_backoff--;
       else if (try_keyed) {
         vm->t2.rec(s);
         r = keyed(used);
-        if (r == 2) r = keyed(used);  // its D table was too small
+        for (int t = 0; r == 2 && t < 3; t++) r = keyed(used);  // its D table / an LRU pool was too small
+        if (r == 2) r = 1;
         if (r < 0) return r;
         if (r == 1) vm->keyed_backoff = kKeyedBackoff;
         if (r == 0) {
@@ -2403,15 +2457,15 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         }
       }
       if (r == 1) {
+        if (ordmaps) vm->ord_backoff = kKeyedBackoff;
         used = XE_MODE_SEQUENTIAL;
         if (int rc = sequential(kms)) return rc;
       }
     } else if (!conflict) {
       vm->keyed_backoff = 0;
+      // the run's results stand: its appends into packet order
+      if (ordmaps && ordered_finalize(vm, ord_h0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
     }
-    // the run's results stand: its appends into packet order
-    if (ordmaps && used == XE_MODE_PARALLEL && ordered_finalize(vm, ord_h0, n, s))
-      return fail(vm, XE_ERR_DEVICE, "ordered map appends");
   }
   vm->keyed_hint = used == XE_MODE_KEYED;
   if (used == XE_MODE_KEYED) red[0] |= XE_FLAG_ORDERED;  // order-dependent effects (shard checks replay it)

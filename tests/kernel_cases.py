@@ -42,6 +42,9 @@ def gpu_cases():
     import test_ordered_par as O
     for build, mdef, entries, _ in O.CASES.values():
         cases.append((build(), [mdef], entries, Settings()))
+    import test_ref_examples as R
+    for prog in (R.from_text(), R.from_literals()):
+        cases.append((prog, [R.STATS_MAP], None, Settings(engine=JIT)))
     return cases
 
 

@@ -14,8 +14,8 @@ import numpy as np
 import pytest
 
 from gobpfld_amd.asm import JEQ, JGT, JNE, Asm
-from gobpfld_amd.emulator import (MAP_LRU_HASH, MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_PARALLEL, MODE_SEQUENTIAL,
-                                  MapDef)
+from gobpfld_amd.emulator import (MAP_LRU_HASH, MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_KEYED, MODE_PARALLEL,
+                                  MODE_SEQUENTIAL, MapDef)
 from parity import assert_same, packets, run_one
 
 
@@ -76,12 +76,33 @@ def prog_lru(update=False):
     return a.assemble()
 
 
+def prog_lru_queue():
+    """LRU learning as prog_lru(update=True), and every packet also pushes its first byte onto a QUEUE
+    (map 2): appends from both keyed passes, put in packet order afterwards."""
+    a = Asm()
+    _head(a, 16)
+    a.ldx(1, 3, 6, 0).stx(8, 10, -24, 3)
+    a.ld_map(1, 2).mov64(2, src=10).add64(2, -24).mov64(3, 0).call(87)
+    a.ldx(1, 3, 6, 0).alu64(0x50, 3, 63).stx(4, 10, -4, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "miss", imm=0)
+    a.mov64(1, 1).xadd(8, 0, 0, 1)
+    a.ja("out")
+    a.label("miss")
+    a.st(8, 10, -16, 7).ld_map(1, 1).mov64(2, src=10).add64(2, -4).mov64(3, src=10).add64(3, -16)
+    a.mov64(4, 0).call(2)
+    a.label("out").mov64(0, 2).exit()
+    return a.assemble()
+
+
 LRU = (MapDef(MAP_LRU_HASH, 4, 8, 64), None)
+LRU_ROOMY = (MapDef(MAP_LRU_HASH, 4, 8, 128), None)  # every key of the stream fits: no eviction
 LRU_PRELOAD = {0: [(k.to_bytes(4, "little"), (1000 * k).to_bytes(8, "little")) for k in range(0, 96, 2)]}
 QUEUE = (MapDef(MAP_QUEUE, 0, 8, 16), None)
 STACK = (MapDef(MAP_STACK, 0, 8, 16), None)
 PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
 PRELOAD = {0: [(None, (0xAB00 + i).to_bytes(8, "little")) for i in range(3)]}  # userspace pushes first
+QUEUE_BIG = (MapDef(MAP_QUEUE, 0, 8, 1 << 20), None)
 
 CASES = {
     "queue": (prog_push, QUEUE, PRELOAD, MODE_PARALLEL),
@@ -90,13 +111,17 @@ CASES = {
     "queue_pop": (lambda: prog_push(pop=True), QUEUE, PRELOAD, MODE_SEQUENTIAL),
     "lru_lookup": (prog_lru, LRU, LRU_PRELOAD, MODE_PARALLEL),
     "lru_update": (lambda: prog_lru(update=True), LRU, LRU_PRELOAD, MODE_SEQUENTIAL),
+    # LRU learning without eviction: the keyed path (misses insert, later packets of the key hit it)
+    "lru_learn": (lambda: prog_lru(update=True), LRU_ROOMY, LRU_PRELOAD, MODE_KEYED),
+    "lru_learn_queue": (prog_lru_queue, LRU_ROOMY, LRU_PRELOAD, MODE_KEYED),
 }
 
 
 def _run(lib, name, n, seed=11):
     build, mdef, entries, _ = CASES[name]
     umem, descs = packets(n, 64, seed=seed)
-    return run_one(lib, build(), [mdef], umem, descs, entries=entries)
+    maps = [mdef] + ([QUEUE_BIG] if name == "lru_learn_queue" else [])
+    return run_one(lib, build(), maps, umem, descs, entries=entries)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))

@@ -38,9 +38,12 @@ WORKLOADS = {
     "c2": "C2 (BASELINE configs[1]): ~40-insn L2/L3 parse->PASS/DROP classifier, per-proto ARRAY counters",
     "c3": "C3: 5-tuple HASH lookup -> REDIRECT + hit counter, 64K flows, IMIX 64/576/1500 B",
     "c4": "C4: ~200-insn JEQ/JGT ACL (48 rules), 1500 B packets, lane-divergence stress",
+    "c4f": "C4 in AF_XDP frames: the C4 ACL over 1500 B packets in 2-KiB UMEM chunks after the 256-byte XDP headroom",
     "c5": "C5: C2 parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets",
     "c3learn": "C3-learn: C3 whose misses (10%, 262,144 new flows) insert the flow (bpf_map_update_elem, BPF_ANY): "
                "map-entry writes, order-dependent; IMIX 64/576/1500 B",
+    "c3lru": "C3-LRU: C3-learn over an LRU_HASH flow table (1M entries, 64K preloaded; every lookup hit and update "
+             "promotes, misses insert; no eviction): keyed chains with the UsageList relinked by last touch",
     "c2rmw": "C2-RMW: C2 with the per-proto counter bumped by a plain load/add/store (value->packets++ without "
              "an atomic): the ordered read-modify-write, run in parallel through lift_rmw",
     "bpf2bpf": "bpf2bpf: call-heavy analogue of the reference's cmd/examples/bpf_to_bpf/src/xdp.c — Ethernet / IPv4 "
@@ -231,27 +234,27 @@ def ordered_paths(d_umem, d_desc, n: int, dev, stream, seq_sample: int = 65536) 
     return out
 
 
-def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536) -> dict:
-    """C3-learn (C3 with flow learning: a miss inserts the flow with bpf_map_update_elem) on fresh map
-    state each run: the keyed ordered execution over all n packets (SPEC pass, chains per written key,
-    xe_internal.h) and, for scale, the one-lane in-order replay (MODE_SEQUENTIAL) on the first
-    `seq_sample` packets. Map upload and kernel compilation stay outside the timed region (a 0-packet
-    run first); the first run of each path is a warm-up."""
+def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536, name: str = "c3learn") -> dict:
+    """C3-learn (C3 with flow learning: a miss inserts the flow with bpf_map_update_elem; "c3lru": the same
+    over an LRU_HASH flow table) on fresh map state each run: the keyed ordered execution over all n
+    packets (SPEC pass, chains per written key, xe_internal.h) and, for scale, the one-lane in-order
+    replay (MODE_SEQUENTIAL) on the first `seq_sample` packets. Map upload and kernel compilation stay
+    outside the timed region (a 0-packet run first); the first run of each path is a warm-up."""
     import torch
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import MODE_SEQUENTIAL, VM, Settings
-    umem, descs = W.build_batch("c3learn", 0, n)
+    umem, descs = W.build_batch(name, 0, n)
     d_umem = torch.from_numpy(umem).to(dev)
     d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
     del umem
-    out = {"program": WORKLOADS["c3learn"]}
+    out = {"program": WORKLOADS[name]}
     for key, mode, cnt, r in (("keyed", 0, n, reps), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
         times, ks, modes, grids = [], [], set(), 0
         for k in range(r + 1):
             vm = VM(Settings(device=dev.index or 0, mode=mode))
-            W.setup_vm(vm, "c3learn")
+            W.setup_vm(vm, name)
             vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), 0, stream=stream)  # upload
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -328,7 +331,7 @@ def shard_truth(name: str, start: int, n: int):
         return np.full(n, 2, np.uint32), None
     if name in ("c2", "c2rmw"):  # C2-RMW: the same counters, bumped by a (lifted) load / add / store
         return _c2_truth(idx)
-    if name == "c4":
+    if name in ("c4", "c4f"):
         return _c4_truth(idx), None
     if name == "c3":
         r0 = W.rng_stream(3, idx, 0)
@@ -570,11 +573,12 @@ def main() -> None:
     if rank == 0 and name == "c2" and not args.no_ordered:
         ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
         ordered["keyed_c3learn"] = keyed_paths(dev, stream, args.keyed_packets)
+        ordered["keyed_c3lru"] = keyed_paths(dev, stream, args.keyed_packets, name="c3lru")
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(name, args.cpu_sample)
-        hw = {"c2": "64B", "c3": "IMIX 64/576/1500B", "c4": "1500B", "c5": "64B"}.get(name, "64B")
+        hw = {"c2": "64B", "c3": "IMIX 64/576/1500B", "c4": "1500B", "c4f": "1500B in 2 KiB frames", "c5": "64B"}.get(name, "64B")
         out = {
             "metric": "Mpkt/s device-resident XDP-emulator verdicts, 64B and 1500B batches",
             "value": round(value, 3),

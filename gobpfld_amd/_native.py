@@ -44,6 +44,16 @@ class PcapInfo(C.Structure):  # include/xdpemu_io.h
                 ("swapped", C.c_uint32), ("first_record", C.c_uint64)]
 
 
+class TraceRec(C.Structure):  # xe_trace_rec: one Step's VM.String (emulator/vm.go:248-270)
+    _fields_ = [("packet", C.c_uint32), ("step", C.c_uint32), ("pc", C.c_int32), ("pi", C.c_int32),
+                ("sf", C.c_uint32), ("kind", C.c_uint8 * 11), ("pad", C.c_uint8), ("val", C.c_int64 * 11)]
+
+
+# xe_helper_fn: int fn(void* user, uint32_t packet, const int64_t args[5], const uint8_t kinds[5], int64_t* r0)
+HELPER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_uint8),
+                        C.POINTER(C.c_int64))
+
+
 class BatchStats(C.Structure):
     _fields_ = [("packets", C.c_uint64), ("steps", C.c_uint64), ("status_count", C.c_uint64 * 8),
                 ("mode_used", C.c_uint32), ("conflict", C.c_uint32), ("kernel_ms", C.c_float),
@@ -59,6 +69,14 @@ def np_dtypes():
                      ("map", "u1", (10,)), ("pad", "u1", (2,)), ("steps", "<u4")], align=True)
     assert desc.itemsize == 16 and result.itemsize == 16 and regs.itemsize == C.sizeof(Regs)
     return desc, result, regs
+
+
+def np_trace_dtype():
+    import numpy as np
+    t = np.dtype([("packet", "<u4"), ("step", "<u4"), ("pc", "<i4"), ("pi", "<i4"), ("sf", "<u4"),
+                  ("kind", "u1", (11,)), ("pad", "u1"), ("val", "<i8", (11,))], align=True)
+    assert t.itemsize == C.sizeof(TraceRec) == 120
+    return t
 
 
 P = C.c_void_p
@@ -84,6 +102,11 @@ _SIGS = {
     "run_batch_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
     "run_batch_device_async": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, P, P, P, P]),
     "sync": (C.c_int, [P]),
+    "cancel": (C.c_int, [P, C.POINTER(C.c_uint32)]),
+    "trace_config": (C.c_int, [P, P, C.c_uint32, C.c_uint32]),
+    "trace_read": (C.c_int, [P, C.c_uint32, P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "set_helper": (C.c_int, [P, C.c_uint32, HELPER_FN, P]),
+    "reset_helper": (C.c_int, [P, C.c_uint32]),
     "prepare": (C.c_int, [P]),
     "debug_set_schedule": (C.c_int, [P, C.c_uint32]),
     "set_kernel_cache": (C.c_int, [C.c_char_p]),
@@ -127,6 +150,7 @@ HEADER_SYMBOLS = [
     "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error", "xe_debug_set_schedule",
     "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source", "xe_kernel_object_name",
+    "xe_cancel", "xe_trace_config", "xe_trace_read", "xe_set_helper", "xe_reset_helper",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h
 

@@ -66,7 +66,7 @@ def sources(cases, lib: N.Lib | None = None, variants=(0, 1, 2)) -> list[str]:
 def bench_cases() -> list:
     """The VMs bench.py and smoke() set up (full-size maps: their geometry is part of the kernel)."""
     from . import workloads as W
-    return [(lambda vm, n=name: W.setup_vm(vm, n)) for name in ("c1", "c2", "c2rmw", "c3", "c3learn", "c4", "c5", "bpf2bpf")]
+    return [(lambda vm, n=name: W.setup_vm(vm, n)) for name in ("c1", "c2", "c2rmw", "c3", "c3learn", "c3lru", "c4", "c5", "bpf2bpf")]
 
 
 def test_sources() -> list[str]:

@@ -52,6 +52,8 @@ enum XeUopClass : uint8_t {
   U_HELPER,     // CallHelper with a known helper id (imm)
   U_CALLX,      // CallHelperIndirect; dst = register holding the helper id
   U_CALLBPF,    // bpf-to-bpf call, emulator/inst_call_bpf.go (general lane model)
+  U_CALLI,      // per-program kernels only: a bpf-to-bpf call inlined (xe_jit.cpp flatten_calls)
+  U_RETI,       // per-program kernels only: the Exit that returns from an inlined call
   U_NCLASSES
 };
 
@@ -367,6 +369,35 @@ struct XeParams {
   // w, w + nwaves, ...; s > 0 = the walk visits chunk (nchunks - 1 - c + s) mod nchunks instead (a
   // permutation; the results may not depend on it)
   uint32_t sched;
+  // instruction trace (xe_trace_config; interpreter engine): the traced packets' batch indices, sorted;
+  // trace_max records per traced packet and the count each run wrote (null trace: off)
+  const uint32_t* trace_pk;
+  xe_trace_rec* trace;
+  uint32_t* trace_cnt;
+  uint32_t trace_npk, trace_max;
+  // helper table (xe_set_helper): bit id of host[] = a host function, of nil[] = a nil entry
+  uint64_t host_helpers[3];
+  uint64_t nil_helpers[3];
+  struct XeHostCall* hostcall;  // the request mailbox (pinned host memory), sequential mode
+};
+
+// Host helper request mailbox (xe_set_helper): the one-lane replay writes the arguments and bumps req
+// (system-scope release); the host thread that runs the batch polls it while the kernel runs, calls the
+// function, writes r0 / err and sets ack = req (release); the lane spins on ack with a time limit.
+#define XE_HOSTCALL_TIMEOUT_TICKS (100ull * 1000 * 1000 * 30)  // 30 s of the 100 MHz constant clock
+struct XeHostCall {
+  uint32_t req;
+  uint32_t ack;
+  uint32_t id;
+  uint32_t packet;
+  int64_t args[5];
+  uint8_t kinds[5];
+  uint8_t pad[3];
+  int32_t err;
+  int64_t r0;
+  // host side only (the host simulation calls the function in place)
+  xe_helper_fn fn[192];
+  void* user[192];
 };
 
 // Decision of the pipelined-batch epilogue (aux word XE_AUX_DECISION): the batch must be replayed in

@@ -201,6 +201,16 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #elif !defined(XE_HAS_ORDERED)
 #define XE_HAS_ORDERED 1
 #endif
+// The VM's helper table (host / nil entries, xe_set_helper) and the instruction trace (xe_trace_config)
+// exist in the interpreter kernel (and the host simulation) only: the runtime does not pick a
+// per-program kernel while either is in use.
+#if XE_GEN && !defined(__HIPCC_RTC__)
+#define XE_HELPER_TABLE 1
+#define XE_TRACE 1
+#else
+#define XE_HELPER_TABLE 0
+#define XE_TRACE 0
+#endif
 
 // Deferred commit (lane_commit, parallel_packets): a chunk's verdict stores and paired-add flush are
 // issued after the next chunk's prefetch instead of at the end of the chunk. The prefetch wait at the
@@ -287,9 +297,16 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #define XE_IS_PANIC(e) (XE_EV_CLASS(e) == XE_EV_PANIC)
 
 #define XE_NOBJ 64
-#define XE_STACK_WORDS 32   // 256-byte frame 0 (fields model)
-#define XE_CTX_WORD0 32     // ctx bytes 0..23 = words 32..34 (fields model)
-#define XE_NWORDS 35
+// Fields model: stack frames 0..XE_NFRAMES-1 (frame f at byte-map words 32 f .. 32 f + 31; more than one
+// when the per-program kernel inlines bpf-to-bpf calls, xe_jit.cpp flatten_calls), then the ctx
+#ifndef XE_NFRAMES
+#define XE_NFRAMES 1
+#endif
+#define XE_STACK_WORDS 32                   // one 256-byte frame
+#define XE_CTX_WORD0 (32 * XE_NFRAMES)      // ctx bytes 0..23 = the three words after the frames
+#define XE_NWORDS (XE_CTX_WORD0 + 3)
+#define XE_DIRTY_WORDS ((XE_NWORDS + 63) / 64)
+static_assert(XE_DIRTY_WORDS <= 4, "fields model: at most 256 byte-map words");
 #define XE_CTX_LEN 24
 #define XE_FRAME 256        // DefaultVMSettings().StackFrameSize (emulator/vm.go:291-296)
 #define XE_MAX_FRAMES 8     // DefaultVMSettings().MaxStackFrames
@@ -314,7 +331,7 @@ XE_DEV uint64_t xe_ctx_default_word(int w) {
 }
 
 // Fields model: the per-program kernel (xe_jit.cpp emit_mem_fields) supplies XeMem as named fields
-// with the xm_* accessors: object ids 1..XE_OBJ_LIMIT-1 (its static bound), 35 byte-map words
+// with the xm_* accessors: object ids 1..XE_OBJ_LIMIT-1 (its static bound), XE_NWORDS byte-map words
 // (frame 0 + ctx, 8 object ids per word).
 #if !XE_GEN
 #define XE_UNROLL_VM _Pragma("unroll")
@@ -366,7 +383,9 @@ struct XeLane {
   // fields above stay splittable into VGPRs)
   struct XeMem* mem;
   uint64_t oused;     // allocated object ids
-  uint64_t dirty;     // ValueMemory words written since Reset
+  // ValueMemory words written since Reset (bit w of the 256-bit mask: word w). Separate scalars, not an
+  // array: a dynamically indexed member array would push the whole lane state to scratch memory.
+  uint64_t dirty0, dirty1, dirty2, dirty3;
 #else
   const XeGen* G;     // arena layout (P.gen, in the kernel-argument segment: scalar loads)
   uint32_t gl;        // this lane's slot in the arena
@@ -493,13 +512,39 @@ XE_DEV void obj_set_val(XeLane& L, int id, int64_t v) {
     xm_set_ov(*L.mem, id, v);
   }
 }
+// A word index the optimiser cannot fold selects among the values, laundered (as the xm_* accessors do):
+// left as plain selects they become one load through a selected address into the lane state, which
+// keeps the whole XeLane out of registers (scratch memory).
+XE_DEV uint64_t dirty_word(const XeLane& L, int w) {  // the dirty-mask word holding bit w
+  if (XE_DIRTY_WORDS == 1) return L.dirty0;
+  if (__builtin_constant_p(w)) return w < 64 ? L.dirty0 : w < 128 ? L.dirty1 : w < 192 ? L.dirty2 : L.dirty3;
+  uint64_t a = L.dirty0, b = L.dirty1, c = L.dirty2, d = L.dirty3;
+#if defined(__HIPCC__)
+  asm("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+#endif
+  return w < 64 ? a : w < 128 ? b : w < 192 ? c : d;
+}
+XE_DEV void dirty_or(XeLane& L, int w, uint64_t bits) {
+  if (XE_DIRTY_WORDS == 1) { L.dirty0 |= bits; return; }
+  L.dirty0 |= w < 64 ? bits : 0ull;
+  L.dirty1 |= w >= 64 && w < 128 ? bits : 0ull;
+  L.dirty2 |= w >= 128 && w < 192 ? bits : 0ull;
+  L.dirty3 |= w >= 192 ? bits : 0ull;
+}
+XE_DEV void dirty_clear(XeLane& L, int w, uint64_t bits) {
+  if (XE_DIRTY_WORDS == 1) { L.dirty0 &= ~bits; return; }
+  L.dirty0 &= w < 64 ? ~bits : ~0ull;
+  L.dirty1 &= w >= 64 && w < 128 ? ~bits : ~0ull;
+  L.dirty2 &= w >= 128 && w < 192 ? ~bits : ~0ull;
+  L.dirty3 &= w >= 192 ? ~bits : ~0ull;
+}
 XE_DEV uint64_t bm_word(const XeLane& L, int w) {
-  if ((L.dirty >> w) & 1ull) return xm_bm(*L.mem, w);
+  if ((dirty_word(L, w) >> (w & 63)) & 1ull) return xm_bm(*L.mem, w);
   return w >= XE_CTX_WORD0 ? xe_ctx_default_word(w) : 0ull;
 }
 XE_DEV void bm_set_word(XeLane& L, int w, uint64_t v) {
   xm_set_bm(*L.mem, w, v);
-  L.dirty |= 1ull << w;
+  dirty_or(L, w, 1ull << (w & 63));
 }
 // the per-program kernel only uses this model when no path can exhaust the ids (xe_jit.cpp)
 XE_DEV int obj_alloc(XeLane& L) {
@@ -509,7 +554,8 @@ XE_DEV int obj_alloc(XeLane& L) {
   return id;
 }
 XE_DEV XeVR vmem_region(const XeLane&, uint32_t h) {
-  return xe_h_cls(h) == XE_H_CTX ? XeVR{XE_CTX_WORD0, XE_CTX_LEN} : XeVR{0, XE_FRAME};
+  return xe_h_cls(h) == XE_H_CTX ? XeVR{XE_CTX_WORD0, XE_CTX_LEN}
+                                  : XeVR{XE_NFRAMES > 1 ? XE_STACK_WORDS * int(xe_h_map(h)) : 0, XE_FRAME};
 }
 XE_DEV int vmem_id(const XeLane& L, XeVR R, int64_t off) {
   uint64_t word = bm_word(L, R.r + int(off >> 3));
@@ -2148,10 +2194,61 @@ XE_COLD int helper_tail_call(XeLane& L, const XeParams& P) {
 }
 #endif
 
+#if XE_HELPER_TABLE
+// A host helper (xe_set_helper, VM.HelperFunctions): R1..R5 go to the host thread that runs the batch
+// through the mailbox, R0 comes back as an IMM. Packet order only (the one-lane path): a parallel pass
+// defers the packet to it.
+XE_COLD int host_helper(XeLane& L, const XeParams& P, uint32_t id) {
+  if (xe_concurrent(P) || !P.hostcall) return XE_EV_ORD;
+  int64_t a[5];
+  uint8_t k[5];
+#pragma unroll
+  for (int r = 0; r < 5; r++) {
+    const XeReg R = reg_get(L, r + 1);
+    a[r] = R.v;
+    k[r] = uint8_t(XE_T_KIND(R.t));
+  }
+  XeHostCall* H = P.hostcall;
+  int32_t err = 0;
+  int64_t r0 = 0;
+#if defined(__HIPCC__)
+  const uint32_t seq = __hip_atomic_load(&H->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+  __hip_atomic_store(&H->id, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&H->packet, L.pidx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+  for (int r = 0; r < 5; r++) {
+    __hip_atomic_store(&H->args[r], a[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    H->kinds[r] = k[r];
+  }
+  __hip_atomic_store(&H->req, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(&H->ack, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    if (wall_clock64() - t0 > XE_HOSTCALL_TIMEOUT_TICKS) return XE_E_HOST_HELPER | XE_E_IN_HELPER;  // nobody served it
+    __builtin_amdgcn_s_sleep(32);
+  }
+  err = __hip_atomic_load(&H->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  r0 = __hip_atomic_load(&H->r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else  // host simulation: the kernel runs on the calling thread, which calls the function in place
+  err = H->fn[id] ? H->fn[id](H->user[id], L.pidx, a, k, &r0) : 1;
+#endif
+  if (err) return XE_E_HOST_HELPER | XE_E_IN_HELPER;
+  reg_replace(L, 0, XE_KIND_IMM, 0, r0, 0);
+  return 0;
+}
+#endif
+
 XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
                        uint32_t cm3 = XE_CM_ALL) {
   if (fn >= 192) return XE_E_NO_HELPER;
   if (fn < 0) return XE_EV_PANIC | XE_P_INDEX;
+#if XE_HELPER_TABLE
+  {
+    const uint32_t w = uint32_t(fn) >> 6;
+    const uint64_t b = 1ull << (uint32_t(fn) & 63u);
+    if (P.nil_helpers[w] & b) return XE_E_NO_HELPER;  // inst_call_helper.go:26-28
+    if (P.host_helpers[w] & b) return host_helper(L, P, uint32_t(fn));
+  }
+#endif
   switch (fn) {
     case 1: return helper_lookup(L, P, cm1, cm2);
     case 2: return helper_update(L, P, cm1, cm2, cm3);
@@ -2237,6 +2334,32 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
   }
   return XE_E_NO_HELPER;
 }
+
+#if !XE_GEN
+// ---- bpf-to-bpf calls inlined into the per-program kernel (fields model; xe_jit.cpp flatten_calls).
+// The generator inlines a call only where R6..R9 can hold just scalars or pointers into a packet the
+// program never writes, so the Registers.Clone the call preserves (registers.go:233-240,294-303) is the
+// value itself with its alias to a stored object dropped; only R6..R9 (and PC) come back at Exit.
+XE_DEV XeReg inl_clone(const XeReg& R) { return XeReg{R.v, R.h, XE_T_KIND(R.t)}; }
+// CallBPF (inst_call_bpf.go:18-44): preserve R6..R9, R10 := the next frame (index f), wiped
+XE_DEV void inl_call(XeLane& L, int f, XeReg& s6, XeReg& s7, XeReg& s8, XeReg& s9) {
+  s6 = inl_clone(reg_get(L, 6));
+  s7 = inl_clone(reg_get(L, 7));
+  s8 = inl_clone(reg_get(L, 8));
+  s9 = inl_clone(reg_get(L, 9));
+  // frame f's 32 words are bits 32 f .. 32 f + 31 of the mask: half of one mask word
+  dirty_clear(L, XE_STACK_WORDS * f, 0xffffffffull << ((XE_STACK_WORDS * f) & 63));
+  reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, uint32_t(f), 0), 0, XE_T_RO);
+}
+// Exit inside a call (inst_exit.go:22-48): R6..R9 from the preserved clones, R10 := the caller's frame f
+XE_DEV void inl_ret(XeLane& L, int f, const XeReg& s6, const XeReg& s7, const XeReg& s8, const XeReg& s9) {
+  reg_put(L, 6, s6);
+  reg_put(L, 7, s7);
+  reg_put(L, 8, s8);
+  reg_put(L, 9, s9);
+  reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, uint32_t(f), 0), 0, XE_T_RO);
+}
+#endif
 
 // ------------------------------------------------------------------ ALU
 XE_DEV int shift_check(int64_t s) { return s < 0 ? (XE_EV_PANIC | XE_P_NEG_SHIFT) : 0; }
@@ -2778,7 +2901,7 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   reg_replace(L, 10, XE_KIND_FRAMEPTR, xe_h_make(XE_H_STACK, 0, 0), 0, XE_T_RO);
   reg_replace(L, 1, XE_KIND_MEMPTR, xe_h_make(XE_H_CTX, 0, 0), 0, 0);
 #if !XE_GEN
-  L.dirty = 0;
+  L.dirty0 = L.dirty1 = L.dirty2 = L.dirty3 = 0;
   L.oused = 0x7full | (XE_OBJ_LIMIT >= 64 ? 0ull : (~0ull << (XE_OBJ_LIMIT & 63)));
 #else
   L.onext = 7;  // ids 1..6: the xdp_md objects
@@ -3332,11 +3455,48 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
 // (valid=false: the lane idles). All lanes of the wave must call this together. A lane's position is
 // (program index, PC): the wave runs the lanes at the smallest index into the concatenated program
 // table, so lanes that tail-called into another program keep their own stream.
+#if XE_TRACE
+// the slot of packet i among the traced packets (sorted), -1 if it is not traced
+XE_DEV int32_t trace_slot(const XeParams& P, uint32_t i) {
+  uint32_t lo = 0, hi = P.trace_npk;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P.trace_pk[mid] < i) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < P.trace_npk && P.trace_pk[lo] == i ? int32_t(lo) : -1;
+}
+// one Step's record: what VM.String prints after it (emulator/vm.go:248-270)
+XE_COLD void trace_put(XeLane& L, const XeParams& P, int32_t slot, uint32_t i, uint64_t step, int32_t pc) {
+  xe_trace_rec r;
+  r.packet = i;
+  r.step = uint32_t(step);
+  r.pc = pc;
+  r.pi = L.pi;
+  r.sf = L.npres;
+  r.pad = 0;
+#pragma unroll 1
+  for (int k = 0; k <= 10; k++) {
+    const XeReg R = reg_get(L, k);
+    r.val[k] = R.v;
+    r.kind[k] = uint8_t(XE_T_KIND(R.t));
+  }
+  P.trace[uint64_t(slot) * P.trace_max + step] = r;
+}
+#endif
+
 XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   int status = valid ? -1 : XE_ST_OK;  // -1 = running
   int code = 0;
   int32_t pc = 0, res_pc = 0;
   uint64_t steps = 0;
+#if XE_GEN
+  L.pidx = i;
+#endif
+#if XE_TRACE
+  const int32_t tslot = valid && P.trace ? trace_slot(P, i) : -1;
+  uint64_t tdone = 0;  // steps that completed
+#endif
 
   for (;;) {
     int key = 0x7fffffff;
@@ -3360,6 +3520,12 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
       int32_t tgt;
       int e = exec_uop(L, P, u, pc, tgt);
       res_pc = pc;
+#if XE_TRACE
+      if (tslot >= 0 && (e == 0 || e == XE_EV_EXIT)) {  // Step returned without an error
+        if (tdone < P.trace_max) trace_put(L, P, tslot, i, tdone, pc);
+        tdone++;
+      }
+#endif
       if (e == 0) {
         if (int64_t(plen) <= int64_t(tgt) + 1) {  // vm.go:162-167
           status = XE_ST_VMERR; code = XE_E_BAD_PC;
@@ -3371,6 +3537,9 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
       }
     }
   }
+#if XE_TRACE
+  if (tslot >= 0) P.trace_cnt[tslot] = uint32_t(tdone < P.trace_max ? tdone : P.trace_max);
+#endif
   lane_finish(L, P, i, valid, status, code, res_pc, steps);
 }
 

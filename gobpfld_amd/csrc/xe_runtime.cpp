@@ -11,12 +11,14 @@
 #include "xe_internal.h"
 
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
 #include <array>
+#include <thread>
 #include <vector>
 
 #ifdef XE_HOSTSIM
@@ -38,7 +40,7 @@ extern "C" int xe_launch_tail(const XeTailArgs* A, hipStream_t s);
 extern "C" int xe_launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* scratch_bytes,
                                       uint32_t* flag, hipStream_t s);
 extern "C" void* xe_jit_get(const XeUop* const* progs, const uint32_t* lens, uint32_t nprogs, int32_t entry, int device,
-                            const XeDevMap* maps, uint32_t nmaps, bool* cyclic, bool* general, const char** err, int keyed);
+                            const XeDevMap* maps, uint32_t nmaps, bool* cyclic, bool* general, const char** err, int keyed, uint64_t* maxpath);
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
@@ -171,6 +173,12 @@ int launch_tail(const XeTailArgs* A, xe_stream_t) {  // xe_kernel.hip xe_tail_ke
 int host_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
 void host_free(void* p) { free(p); }
 int host_device_ptr(void** d, void* h) { *d = h; return 0; }
+int host_alloc_coherent(void** p, size_t n) { return host_alloc(p, n); }
+// host helpers: the simulated kernel ran on this thread and called them in place
+int serve_hostcalls(XeHostCall*, xe_stream_t) { return 0; }
+// xe_cancel: the simulated batches are complete when their call returns
+int poison_async(uint32_t* d, xe_stream_t*) { *d = 2; return 0; }
+void stream_destroy(xe_stream_t) {}
 int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
                         xe_stream_t) {  // xe_kernel.hip xe_launch_desc_overlap
   if (!scratch) { *bytes = 8; return 0; }
@@ -287,6 +295,43 @@ int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* s
 }
 // device-visible address of pinned host memory (hipHostMalloc default: mapped, coherent)
 int host_device_ptr(void** d, void* h) { return hipHostGetDevicePointer(d, h, 0) == hipSuccess ? 0 : -1; }
+// pinned host memory the device polls with system-scope atomics (the host helper mailbox)
+int host_alloc_coherent(void** p, size_t n) {
+  if (hipHostMalloc(p, n ? n : 8, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return -1;
+  memset(*p, 0, n);
+  return 0;
+}
+// Host helpers (xe_set_helper): until the batch's stream is idle, answer the one-lane replay's requests
+// in the mailbox (the lane waits for ack == req), calling the registered function on this thread.
+int serve_hostcalls(XeHostCall* H, xe_stream_t s) {
+  for (;;) {
+    const uint32_t req = __atomic_load_n(&H->req, __ATOMIC_ACQUIRE);
+    if (req != __atomic_load_n(&H->ack, __ATOMIC_RELAXED)) {
+      const uint32_t id = H->id;
+      int64_t a[5];
+      uint8_t k[5];
+      for (int r = 0; r < 5; r++) { a[r] = H->args[r]; k[r] = H->kinds[r]; }
+      int64_t r0 = 0;
+      const int err = (id < 192 && H->fn[id]) ? H->fn[id](H->user[id], H->packet, a, k, &r0) : 1;
+      H->r0 = r0;
+      H->err = err ? 1 : 0;
+      __atomic_store_n(&H->ack, req, __ATOMIC_RELEASE);
+      continue;
+    }
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return -1;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+// xe_cancel: mark the pipelined batches poisoned from a stream of its own, so the batches still queued
+// behind the running one see it at their first wave (the VM's stream would run the write after them)
+int poison_async(uint32_t* d, xe_stream_t* cs) {
+  if (!*cs && hipStreamCreateWithFlags(cs, hipStreamNonBlocking) != hipSuccess) return -1;
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d), 2u, 1, *cs) != hipSuccess) return -1;
+  return hipStreamSynchronize(*cs) == hipSuccess ? 0 : -1;
+}
+void stream_destroy(xe_stream_t s) { if (s) (void)hipStreamDestroy(s); }
 struct Timer {
   hipEvent_t e = nullptr;
   void init() { if (!e) (void)hipEventCreate(&e); }
@@ -554,7 +599,9 @@ struct HostMap {
   uint32_t* d_state = nullptr;
   uint32_t* d_count = nullptr;
   uint8_t* d_snap = nullptr;
-  std::array<uint8_t*, kAsyncDepth> d_asnap{};  // rollback points of the pipelined batches in flight
+  // rollback points of the pipelined batches in flight: one more than the batches in flight, so the
+  // newest batch's epilogue (which stages its successor's) never overwrites the oldest batch's (xe_cancel)
+  std::array<uint8_t*, kAsyncDepth + 1> d_asnap{};
   uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
   uint32_t nrep = 1;
   uint64_t rep_stride = 0;
@@ -715,6 +762,7 @@ struct xe_vm {
   size_t jit_nprogs = 0;  // programs of the VM when the kernel was built (tail calls compile them all in)
   void* jit_fn = nullptr;
   bool jit_cyclic = false;
+  uint64_t jit_maxpath = 0;  // acyclic kernels: the most instructions a packet can execute
   bool jit_general = false;  // the per-program kernel uses the general lane model (loops, > 57 objects)
   std::string jit_error;
   // its keyed variant (keyed ordered execution), built with it when the program may write map entries
@@ -742,13 +790,16 @@ struct xe_vm {
     Batch b;
     size_t aux_used = 0;
     uint32_t nmaps = 0, grid = 0, engine = 0;
+    uint32_t snap = 0;  // index of the batch's rollback point (HostMap::d_asnap)
   };
   std::array<Slot, kAsyncDepth> slots;
   std::vector<uint32_t> pending;
   uint32_t next_slot = 0;
+  uint32_t next_snap = 0;  // rollback point of the next pipelined batch
   uint32_t* d_poison = nullptr;
-  // slot whose small-map snapshots the last pipelined batch's tail wrote (-1: none valid); anything
-  // else that writes device map values invalidates it (stage_invalidate)
+  xe_stream_t cancel_stream = nullptr;  // xe_cancel's write of the poison word (non-blocking stream)
+  // rollback point (HostMap::d_asnap index) the last pipelined batch's tail staged for its successor
+  // (-1: none valid); anything else that writes device map values invalidates it
   int32_t staged_slot = -1;
   bool draining = false;
   bool delta_base = true;  // the map snapshots are the start of the last batch (false after async batches)
@@ -772,6 +823,19 @@ struct xe_vm {
   // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
   // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
   uint32_t keyed_backoff = 0;
+  // instruction trace (xe_trace_config): the traced packets (sorted), records kept per packet, device
+  // copies (records, per-packet counts)
+  std::vector<uint32_t> trace_pk;
+  uint32_t trace_max = 0;
+  uint32_t* d_trace_pk = nullptr;
+  xe_trace_rec* d_trace = nullptr;
+  uint32_t* d_trace_cnt = nullptr;
+  // helper table (xe_set_helper): host functions and nil entries; the request mailbox (pinned host
+  // memory, allocated with the first host function) and its device-visible address
+  uint64_t host_helpers[3] = {0, 0, 0};
+  uint64_t nil_helpers[3] = {0, 0, 0};
+  XeHostCall* h_hostcall = nullptr;
+  XeHostCall* d_hostcall = nullptr;
   // ordered maps: after a parallel try of a batch had to be replayed in order, the next kKeyedBackoff
   // batches replay straight away; scratch of the append ordering (XeAppendArgs)
   uint32_t ord_backoff = 0;
@@ -1333,6 +1397,9 @@ void xe_destroy(xe_vm* vm) {
     sl.t0.fini(); sl.t1.fini(); sl.done.fini();
   }
   dev_free(vm->d_poison);
+  stream_destroy(vm->cancel_stream);
+  dev_free(vm->d_trace_pk); dev_free(vm->d_trace); dev_free(vm->d_trace_cnt);
+  host_free(vm->h_hostcall);
   for (auto& m : vm->maps) map_free_device(m);
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
@@ -1513,6 +1580,42 @@ int xe_map_update_batch(xe_vm* vm, int32_t mi, const void* keys, const void* val
   HostMap* m = get_map(vm, mi);
   if (!m || (count && (!keys || !values))) return XE_ERR_INVAL;
   const size_t ks = m->dkind == XE_DM_ARRAY ? 4 : m->def.key_size, vs = m->def.value_size;
+  if (m->dkind == XE_DM_LRU && count > 1) {
+    // The updates one by one leave every updated key ahead of the others, the last updated first, each
+    // holding its last value (maps_hash_lru.go:93-161: every Update promotes): built directly when nothing
+    // is evicted on the way (the keys already present plus the new ones fit MaxEntries).
+    set_device(vm->settings.device);
+    if (map_download(vm, *m)) return fail(vm, XE_ERR_DEVICE, "map download");
+    std::map<std::vector<uint8_t>, size_t> pos;
+    for (size_t i = 0; i < m->items.size(); i++)
+      if (!m->items[i].nil_key) pos[m->items[i].key] = i;
+    std::map<std::vector<uint8_t>, uint64_t> last;
+    for (uint64_t i = 0; i < count; i++) {
+      const uint8_t* k = (const uint8_t*)keys + i * ks;
+      last[std::vector<uint8_t>(k, k + ks)] = i;
+    }
+    uint64_t fresh = 0;
+    for (const auto& kv : last) fresh += pos.count(kv.first) ? 0 : 1;
+    if (m->items.size() + fresh <= m->def.max_entries) {
+      std::vector<std::pair<uint64_t, const std::vector<uint8_t>*>> order;
+      for (const auto& kv : last) order.push_back({kv.second, &kv.first});
+      std::sort(order.begin(), order.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+      std::vector<HostMap::Rec> items;
+      items.reserve(m->items.size() + fresh);
+      for (const auto& o : order) {
+        HostMap::Rec r;
+        r.key = *o.second;
+        const uint8_t* v = (const uint8_t*)values + o.first * vs;
+        r.val.assign(v, v + vs);
+        items.push_back(std::move(r));
+      }
+      for (auto& r : m->items)
+        if (r.nil_key || !last.count(r.key)) items.push_back(std::move(r));
+      m->items = std::move(items);
+      m->host_dirty = true;
+      return XE_OK;
+    }
+  }
   for (uint64_t i = 0; i < count; i++)
     if (int rc = xe_map_update(vm, mi, (const uint8_t*)keys + i * ks, (const uint8_t*)values + i * vs)) return rc;
   return XE_OK;
@@ -1652,9 +1755,21 @@ static bool may_write_packet(const std::vector<XeUop>& prog) {
         auto reg = [&](int x) -> uint8_t { return x <= 10 ? r[x] : 0; };
         auto set = [&](int x, uint8_t v) { if (x <= 10) r[x] = v; };
         int succ[2] = {int(pc) + 1, -1};
+        std::array<uint8_t, 11> after = {};  // a call's fall-through: the state the callee returns with
+        bool call = false;
         switch (u.cls) {
           case U_FAIL: case U_EXIT: succ[0] = -1; break;
-          case U_CALLBPF: case U_CALLX: return true;  // not analysed: be conservative
+          case U_CALLX: return true;  // not analysed: be conservative
+          case U_CALLBPF:
+            // the callee starts from the caller's registers in a new frame; back after the call, R6..R9
+            // are the caller's (inst_exit.go:22-48) and R0..R5 whatever the callee left: anything
+            call = true;
+            after = r;
+            for (int x = 0; x <= 5; x++) after[x] = T_PKT | T_CTX | T_FRM;
+            r[10] = T_FRM;
+            succ[0] = int(pc) + u.imm + 1;
+            succ[1] = int(pc) + 1;
+            break;
           case U_JA: succ[0] = u.tgt + 1; break;
           case U_JMP: succ[1] = u.tgt + 1; break;
           case U_MOVI: set(u.dst, 0); break;
@@ -1680,7 +1795,8 @@ static bool may_write_packet(const std::vector<XeUop>& prog) {
           const int t = succ[k];
           if (t < 0 || t >= int(n)) continue;
           std::array<uint8_t, 11> m = in[t];
-          for (int x = 0; x <= 10; x++) m[x] |= r[x];
+          const std::array<uint8_t, 11>& src = (call && k == 1) ? after : r;
+          for (int x = 0; x <= 10; x++) m[x] |= src[x];
           if (!reach[t] || m != in[t]) { in[t] = m; reach[t] = true; changed = true; }
         }
       }
@@ -1889,6 +2005,26 @@ static int ensure_arena(xe_vm* vm, bool seq, uint32_t nl, XeGen& g) {
 
 namespace {
 
+// The helper table differs from LinuxHelperFunctions (xe_set_helper) or a trace is configured: both live in
+// the interpreter kernel only (xe_interp.h XE_HELPER_TABLE / XE_TRACE).
+bool interp_only(const xe_vm* vm) {
+  return (vm->host_helpers[0] | vm->host_helpers[1] | vm->host_helpers[2] | vm->nil_helpers[0] | vm->nil_helpers[1] |
+          vm->nil_helpers[2]) != 0 ||
+         !vm->trace_pk.empty();
+}
+
+// Some program of the VM may call a host function (directly, or through CallHelperIndirect): its batches
+// run in packet order on one lane, the only place a host function is called.
+bool calls_host_helper(const xe_vm* vm) {
+  if (!(vm->host_helpers[0] | vm->host_helpers[1] | vm->host_helpers[2])) return false;
+  for (size_t q = 1; q < vm->programs.size(); q++)
+    for (const XeUop& u : vm->programs[q]) {
+      if (u.cls == U_CALLX) return true;
+      if (u.cls == U_HELPER && u.imm >= 0 && u.imm < 192 && ((vm->host_helpers[u.imm >> 6] >> (u.imm & 63)) & 1)) return true;
+    }
+  return false;
+}
+
 // launch parameters of a batch (flags / replica records at aux)
 XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n, void* d_results,
                       void* d_verdicts, void* d_regs, unsigned long long* aux) {
@@ -1917,6 +2053,18 @@ XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_
   P.nrep = kRep;
   P.rep_words = 16 + 2 * (P.nmaps + 1);
   P.sched = vm->sched;
+  if (!vm->trace_pk.empty()) {
+    P.trace_pk = vm->d_trace_pk;
+    P.trace = vm->d_trace;
+    P.trace_cnt = vm->d_trace_cnt;
+    P.trace_npk = uint32_t(vm->trace_pk.size());
+    P.trace_max = vm->trace_max;
+  }
+  for (int w = 0; w < 3; w++) {
+    P.host_helpers[w] = vm->host_helpers[w];
+    P.nil_helpers[w] = vm->nil_helpers[w];
+  }
+  P.hostcall = vm->d_hostcall;
   return P;
 }
 
@@ -1925,16 +2073,18 @@ XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_
 int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
   jit = nullptr;
   jit_general = false;
-#ifndef XE_HOSTSIM
   const uint32_t engine = vm->settings.engine;
-  if (engine != XE_ENGINE_INTERP && jit_possible(vm)) {
+  if (engine == XE_ENGINE_JIT && interp_only(vm))
+    return fail(vm, XE_ERR_UNSUPPORTED, "a changed helper table or an instruction trace needs the interpreter engine");
+#ifndef XE_HOSTSIM
+  if (engine != XE_ENGINE_INTERP && jit_possible(vm) && !interp_only(vm)) {
     if (vm->jit_idx != vm->entry || vm->jit_nmaps != vm->maps.size() || vm->jit_nprogs != vm->programs.size()) {
       // the kernel is specialised on the program and the map geometry (xe_jit.cpp)
       const ProgTab t = prog_tab(vm);
       const char* jerr = "";
       vm->jit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
                               vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &vm->jit_cyclic,
-                              &vm->jit_general, &jerr, 0);
+                              &vm->jit_general, &jerr, 0, &vm->jit_maxpath);
       vm->jit_error = jerr ? jerr : "";
       vm->jit_idx = vm->entry;
       vm->jit_nmaps = vm->maps.size();
@@ -1947,7 +2097,7 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
     jit = vm->jit_fn;
     jit_general = vm->jit_general;
     // acyclic kernels carry no budget checks: exact only while the budget cannot be reached
-    if (jit && !vm->jit_cyclic && vm->settings.max_steps < vm->d_prog_len) jit = nullptr;
+    if (jit && !vm->jit_cyclic && vm->settings.max_steps < std::max<uint64_t>(vm->d_prog_len, vm->jit_maxpath)) jit = nullptr;
   }
   if (!jit && engine == XE_ENGINE_JIT) return fail(vm, XE_ERR_DEVICE, "JIT engine unavailable: " + vm->jit_error);
 #endif
@@ -1966,7 +2116,7 @@ void* keyed_kernel(xe_vm* vm, void* jit) {
     bool cy = false, ge = false;
     const char* jerr = "";
     vm->kjit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
-                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1);
+                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 1, nullptr);
     vm->kjit_ready = true;
   }
   return vm->kjit_fn;
@@ -1986,7 +2136,7 @@ void* lean_kernel(xe_vm* vm, void* jit) {
     bool cy = false, ge = false;
     const char* jerr = "";
     vm->ljit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
-                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 2);
+                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 2, nullptr);
     vm->ljit_ready = true;
   }
   return vm->ljit_fn ? vm->ljit_fn : jit;
@@ -2082,6 +2232,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
 
   XeParams P = batch_params(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, vm->d_aux);
   const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+  if (P.trace && dmemset(vm->d_trace_cnt, 0, vm->trace_pk.size() * 4, s)) return fail(vm, XE_ERR_DEVICE, "trace reset");
+  // host functions are called in packet order only
+  const bool hostcalls = calls_host_helper(vm);
 
   const uint32_t mode = vm->settings.mode;
   void* jit = nullptr;
@@ -2190,6 +2343,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       vm->t1.rec(s);
       if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t2.rec(s);
+      if (hostcalls && serve_hostcalls(vm->h_hostcall, s)) return fail(vm, XE_ERR_DEVICE, "kernel failed (host helpers)");
       if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
       ms += Timer::ms(vm->t1, vm->t2);
       if (!(red[0] & XE_FLAG_CAPACITY)) return XE_OK;
@@ -2386,7 +2540,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   bool ord_seq = mode == XE_MODE_AUTO && ordmaps && (!ord_par || vm->ord_backoff);
   if (ord_seq && vm->ord_backoff) vm->ord_backoff--;
   std::vector<uint64_t> ord_h0;
-  if (mode == XE_MODE_SEQUENTIAL || ord_seq || overlap) {
+  if (mode == XE_MODE_SEQUENTIAL || ord_seq || overlap || hostcalls) {
     used = XE_MODE_SEQUENTIAL;
     if (int rc = sequential(kms)) return rc;
   } else if (keyed_ok && vm->keyed_hint) {
@@ -2513,7 +2667,7 @@ int complete_oldest(xe_vm* vm) {
     const xe_stream_t s = sl.b.s;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
-      if (!m.ordered() && d2d(m.d_vals, m.d_asnap[si], m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      if (!m.ordered() && d2d(m.d_vals, m.d_asnap[sl.snap], m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
     }
     if (dmemset(vm->d_poison, 0, 4, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
     std::vector<xe_vm::Batch> redo;
@@ -2600,6 +2754,117 @@ int xe_sync(xe_vm* vm) {
   return XE_OK;
 }
 
+// RunContext's ctx.Err() (emulator/vm.go:117-134) for the pipelined batches: drop every batch not
+// completed yet. The poison word makes the queued launches return at their first wave; the maps go back
+// to the oldest dropped batch's rollback point (the snapshot its prologue or its predecessor's epilogue
+// took before it ran), with the value replicas cleared.
+int xe_cancel(xe_vm* vm, uint32_t* cancelled) {
+  if (!vm) return XE_ERR_INVAL;
+  if (cancelled) *cancelled = 0;
+  if (vm->pending.empty()) return XE_OK;
+  set_device(vm->settings.device);
+  const uint32_t si = vm->pending.front();
+  const xe_stream_t s = vm->slots[si].b.s;
+  if (poison_async(vm->d_poison, &vm->cancel_stream) || dsync(s)) {
+    vm->pending.clear();
+    return fail(vm, XE_ERR_DEVICE, "cancel");
+  }
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    if (m.ordered()) continue;  // (maps of this kind never pipeline)
+    if (d2d(m.d_vals, m.d_asnap[vm->slots[si].snap], m.vals_alloc, s)) return fail(vm, XE_ERR_DEVICE, "cancel (rollback)");
+    if (m.nrep > 1 && m.d_rep && dmemset(m.d_rep, 0, m.rep_stride * m.nrep, s)) return fail(vm, XE_ERR_DEVICE, "cancel");
+  }
+  for (uint32_t k : vm->pending) {
+    xe_vm::Slot& sl = vm->slots[k];
+    if (dmemset(sl.d_aux, 0, kAuxWords * 8, s)) return fail(vm, XE_ERR_DEVICE, "cancel");
+    if (xe_batch_stats* st = sl.b.stats) {
+      memset(st, 0, sizeof *st);
+      st->packets = sl.b.n;
+      st->mode_used = XE_MODE_CANCELLED;
+      st->engine_used = sl.engine;
+      st->grid_blocks = sl.grid;
+    }
+  }
+  if (cancelled) *cancelled = uint32_t(vm->pending.size());
+  vm->pending.clear();
+  vm->staged_slot = -1;
+  if (dmemset(vm->d_poison, 0, 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "cancel");
+  return XE_OK;
+}
+
+int xe_trace_config(xe_vm* vm, const uint32_t* packets, uint32_t npk, uint32_t max_steps) {
+  if (!vm || (npk && !packets) || npk > XE_TRACE_MAX_PACKETS || max_steps > XE_TRACE_MAX_STEPS) return XE_ERR_INVAL;
+  if (npk && !max_steps) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  set_device(vm->settings.device);
+  dev_free(vm->d_trace_pk); dev_free(vm->d_trace); dev_free(vm->d_trace_cnt);
+  vm->d_trace_pk = nullptr; vm->d_trace = nullptr; vm->d_trace_cnt = nullptr;
+  vm->trace_pk.assign(packets, packets + npk);
+  std::sort(vm->trace_pk.begin(), vm->trace_pk.end());
+  vm->trace_pk.erase(std::unique(vm->trace_pk.begin(), vm->trace_pk.end()), vm->trace_pk.end());
+  vm->trace_max = npk ? max_steps : 0;
+  if (vm->trace_pk.empty()) return XE_OK;
+  const size_t k = vm->trace_pk.size();
+  if (dev_alloc((void**)&vm->d_trace_pk, k * 4) || dev_alloc((void**)&vm->d_trace, k * max_steps * sizeof(xe_trace_rec)) ||
+      dev_alloc((void**)&vm->d_trace_cnt, k * 4) || h2d(vm->d_trace_pk, vm->trace_pk.data(), k * 4, vm->stream) ||
+      dmemset(vm->d_trace_cnt, 0, k * 4, vm->stream) || dsync(vm->stream)) {
+    vm->trace_pk.clear();
+    return fail(vm, XE_ERR_NOMEM, "device alloc (trace)");
+  }
+  return XE_OK;
+}
+
+int xe_trace_read(xe_vm* vm, uint32_t packet, xe_trace_rec* out, uint32_t cap, uint32_t* nsteps) {
+  if (!vm || !nsteps) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  auto it = std::lower_bound(vm->trace_pk.begin(), vm->trace_pk.end(), packet);
+  if (it == vm->trace_pk.end() || *it != packet) return fail(vm, XE_ERR_INVAL, "packet is not traced");
+  const size_t slot = size_t(it - vm->trace_pk.begin());
+  set_device(vm->settings.device);
+  uint32_t cnt = 0;
+  if (d2h(&cnt, vm->d_trace_cnt + slot, 4, vm->stream) || dsync(vm->stream)) return fail(vm, XE_ERR_DEVICE, "trace read");
+  *nsteps = cnt;
+  if (!out || !cap) return XE_OK;
+  const uint32_t c = std::min(cap, cnt);
+  if (c && (d2h(out, vm->d_trace + slot * vm->trace_max, size_t(c) * sizeof(xe_trace_rec), vm->stream) || dsync(vm->stream)))
+    return fail(vm, XE_ERR_DEVICE, "trace read");
+  return XE_OK;
+}
+
+int xe_set_helper(xe_vm* vm, uint32_t id, xe_helper_fn fn, void* user) {
+  if (!vm || id >= 192) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  const uint64_t b = 1ull << (id & 63);
+  if (fn) {
+    if (!vm->h_hostcall) {
+      set_device(vm->settings.device);
+      void* h = nullptr;
+      void* d = nullptr;
+      if (host_alloc_coherent(&h, sizeof(XeHostCall)) || host_device_ptr(&d, h)) return fail(vm, XE_ERR_NOMEM, "host helper mailbox");
+      vm->h_hostcall = (XeHostCall*)h;
+      vm->d_hostcall = (XeHostCall*)d;
+    }
+    vm->h_hostcall->fn[id] = fn;
+    vm->h_hostcall->user[id] = user;
+    vm->host_helpers[id >> 6] |= b;
+    vm->nil_helpers[id >> 6] &= ~b;
+  } else {
+    vm->host_helpers[id >> 6] &= ~b;
+    vm->nil_helpers[id >> 6] |= b;
+  }
+  return XE_OK;
+}
+
+int xe_reset_helper(xe_vm* vm, uint32_t id) {
+  if (!vm || id >= 192) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  const uint64_t b = 1ull << (id & 63);
+  vm->host_helpers[id >> 6] &= ~b;
+  vm->nil_helpers[id >> 6] &= ~b;
+  return XE_OK;
+}
+
 int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                               void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
@@ -2609,7 +2874,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   // batches that cannot pipeline run synchronously, after everything in flight
   // (keyed_hint: the last batch wrote map entries, this one starts with the keyed path's SPEC pass)
   if (!entry_ok || vm->settings.mode == XE_MODE_SEQUENTIAL || has_ordered_maps(vm) || vm->keyed_hint ||
-      (umem_len && may_write_packet(vm->programs[vm->entry])))
+      (umem_len && may_write_packet(vm->programs[vm->entry])) || !vm->trace_pk.empty() || calls_host_helper(vm))
     return xe_run_batch_device(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, stream, stats);
   if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
   // the pipeline is stream order: a batch on another stream waits for the ones in flight
@@ -2626,7 +2891,8 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   if (int rc = select_engine(vm, jit, jit_general)) return rc;
   const bool general = !jit || jit_general;
 
-  const uint32_t si = vm->next_slot, nsi = (si + 1) % kAsyncDepth;
+  const uint32_t si = vm->next_slot;
+  const uint32_t ai = vm->next_snap, nai = (ai + 1) % (kAsyncDepth + 1);  // its rollback point, the next one's
   xe_vm::Slot& sl = vm->slots[si];
   if (!sl.d_aux) {  // the slot's records start zeroed; every batch epilogue zeroes them again
     if (dev_alloc((void**)&sl.d_aux, kAuxWords * 8) || dmemset(sl.d_aux, 0, kAuxWords * 8, s))
@@ -2647,7 +2913,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   // small maps are folded and snapshotted for the next batch there too, the others keep the
   // prologue snapshot and their own fold launch. This batch's rollback point: the snapshot the
   // previous batch's epilogue staged, when nothing has written the maps since.
-  const bool staged = vm->staged_slot == int32_t(si) && !vm->pending.empty() && vm->slots[vm->pending.back()].b.s == s;
+  const bool staged = vm->staged_slot == int32_t(ai) && !vm->pending.empty() && vm->slots[vm->pending.back()].b.s == s;
   XeTailArgs A{};
   A.aux = sl.d_aux;
   A.host_aux = sl.h_aux_dev;
@@ -2663,7 +2929,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   std::vector<size_t> big;  // maps folded by their own launch
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
-    for (uint32_t k : {si, nsi})
+    for (uint32_t k : {ai, nai})
       if (!m.d_asnap[k] && dev_alloc((void**)&m.d_asnap[k], m.vals_alloc))
         return fail(vm, XE_ERR_DEVICE, "device alloc (batch snapshot)");
     const bool small = m.vals_alloc <= kTailMapBytes && A.ntail < XE_TAIL_MAPS;
@@ -2671,7 +2937,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
       XeTailMap& T = A.tail[A.ntail++];
       T.vals = (unsigned long long*)m.d_vals;
       T.rep = (unsigned long long*)m.d_rep;
-      T.snap = (unsigned long long*)m.d_asnap[nsi];
+      T.snap = (unsigned long long*)m.d_asnap[nai];
       T.words = m.vals_alloc / 8;
       T.stride_words = m.rep_stride / 8;
       T.nrep = m.nrep > 1 ? m.nrep : 0;
@@ -2680,7 +2946,7 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
     }
     if (!small || !staged) {
       src.push_back(m.d_vals);
-      dst.push_back(m.d_asnap[si]);
+      dst.push_back(m.d_asnap[ai]);
       words.push_back(m.vals_alloc / 8);
     }
   }
@@ -2699,7 +2965,9 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
   }
   if (launch_tail(&A, s)) return fail(vm, XE_ERR_DEVICE, "epilogue");
   sl.done.rec(s);
-  vm->staged_slot = int32_t(nsi);
+  vm->staged_slot = int32_t(nai);
+  sl.snap = ai;
+  vm->next_snap = nai;
   sl.b = xe_vm::Batch{d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, s, stats};
   sl.aux_used = aux_used;
   sl.nmaps = P.nmaps;

@@ -27,6 +27,8 @@ ARRAY_TYPES = (MAP_ARRAY, MAP_PERCPU_ARRAY, MAP_PROG_ARRAY, MAP_ARRAY_OF_MAPS)
 HASH_TYPES = (MAP_HASH, MAP_PERCPU_HASH, MAP_HASH_OF_MAPS, MAP_LRU_HASH, MAP_LRU_PERCPU_HASH)
 LIST_TYPES = (MAP_QUEUE, MAP_STACK, MAP_PERF_EVENT_ARRAY)
 MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL, MODE_KEYED = 0, 1, 2, 3  # MODE_KEYED: mode_used only
+MODE_CANCELLED = 4  # mode_used of a pipelined batch VM.cancel dropped
+E_HOST_HELPER, E_IN_HELPER = 17, 0x80
 ENGINE_AUTO, ENGINE_INTERP, ENGINE_JIT = 0, 1, 2
 
 
@@ -84,6 +86,12 @@ def initial_image(d: MapDef, data: dict) -> bytes | None:
     return bytes(img)
 
 
+def _wrap64(v: int) -> int:
+    """a Python int as the int64 R0 a helper returns (two's complement wrap)"""
+    v = int(v) & ((1 << 64) - 1)
+    return v - (1 << 64) if v >> 63 else v
+
+
 def _stats_dict(s: N.BatchStats) -> dict:
     return {"packets": s.packets, "steps": s.steps, "status_count": list(s.status_count),
             "mode_used": s.mode_used, "conflict": s.conflict, "kernel_ms": s.kernel_ms,
@@ -118,6 +126,7 @@ class VM:
         self.h = h
         self.map_defs: dict[int, MapDef] = {}
         self._pending: list = []  # pipelined batches whose statistics the library still writes
+        self._helpers: dict[int, object] = {}  # ctypes callbacks of the host helpers (kept alive)
 
     def close(self) -> None:
         if self.h:
@@ -323,6 +332,57 @@ class VM:
         rc = self.lib.sync(self.h)
         self._pending.clear()
         self._check(rc, "sync")
+
+    def cancel(self) -> int:
+        """xe_cancel (RunContext's cancellation, emulator/vm.go:117-134): drop every pipelined batch not
+        completed yet; the maps return to the state before the oldest of them. Returns how many."""
+        k = C.c_uint32()
+        rc = self.lib.cancel(self.h, C.byref(k))
+        self._pending.clear()
+        self._check(rc, "cancel")
+        return k.value
+
+    # ---- Step / VM.String: per-packet instruction trace
+    def trace(self, packets, max_steps: int = 256) -> None:
+        """xe_trace_config: record the first max_steps Steps of each listed packet of every batch
+        ([] turns it off)."""
+        arr = np.ascontiguousarray(np.asarray(list(packets), dtype=np.uint32))
+        self._check(self.lib.trace_config(self.h, arr.ctypes.data if len(arr) else None, len(arr),
+                                          max_steps if len(arr) else 0), "trace config")
+
+    def trace_read(self, packet: int) -> np.ndarray:
+        """The Step records of `packet` in the last batch (N.np_trace_dtype(): pc, pi, sf, kind[11], val[11])."""
+        n = C.c_uint32()
+        self._check(self.lib.trace_read(self.h, packet, None, 0, C.byref(n)), "trace read")
+        out = np.zeros(n.value, dtype=N.np_trace_dtype())
+        if n.value:
+            self._check(self.lib.trace_read(self.h, packet, out.ctypes.data, n.value, C.byref(n)), "trace read")
+        return out
+
+    # ---- the helper table (VM.HelperFunctions)
+    def set_helper(self, hid: int, fn) -> None:
+        """Replace helper `hid` (emulator/helper_functions.go:17 HelperFunc): fn(packet, args[5], kinds[5])
+        returns R0 (an int) or raises to abort the packet (XE_E_HOST_HELPER); fn=None makes the entry nil."""
+        if fn is None:
+            self._check(self.lib.set_helper(self.h, hid, N.HELPER_FN(), None), "set helper")
+            self._helpers.pop(hid, None)
+            return
+
+        def tramp(_user, packet, args, kinds, r0):
+            try:
+                r0[0] = _wrap64(fn(int(packet), [args[i] for i in range(5)], [kinds[i] for i in range(5)]))
+                return 0
+            except Exception:
+                return 1
+
+        cb = N.HELPER_FN(tramp)
+        self._check(self.lib.set_helper(self.h, hid, cb, None), "set helper")
+        self._helpers[hid] = cb
+
+    def reset_helper(self, hid: int) -> None:
+        """Entry `hid` back to LinuxHelperFunctions' (the built-in helper or nil)."""
+        self._check(self.lib.reset_helper(self.h, hid), "reset helper")
+        self._helpers.pop(hid, None)
 
     # ---- multi-GPU shard support
     def map_delta(self, m: int, d_out: int, stream: int = 0, lane: int = 0) -> None:

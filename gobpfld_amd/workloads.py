@@ -10,6 +10,8 @@ regenerates identical packets; seed_c = 0x6F62706C64000000 + c.
   C5  C2-style parse + per-flow HASH counters {pkts, bytes}, 1M flows, 64 B packets, sharded
   C3-learn  C3 with flow learning: a miss inserts the flow (bpf_map_update_elem) — map-entry writes,
             order-dependent (the keyed path, xe_internal.h XE_MODE_SPEC / XE_MODE_CHAIN)
+  C3-LRU    C3-learn over an LRU_HASH flow table (every lookup and update promotes; no eviction: the
+            keyed path with the UsageList relinked by last touch)
 
 All programs avoid JLT/JLE/JSET (rejected by emulator/inst.go Translate) and use only helper 1
 (map lookup) — bpf_redirect does not exist in the reference emulator, so REDIRECT is `r0 = 4`.
@@ -21,7 +23,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .asm import (Asm, JEQ, JGT, JNE, XDP_DROP, XDP_PASS, XDP_REDIRECT)
-from .emulator import MAP_ARRAY, MAP_HASH, MapDef
+from .emulator import MAP_ARRAY, MAP_HASH, MAP_LRU_HASH, MapDef
 
 SEED0 = 0x6F62706C64000000
 M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
@@ -515,7 +517,11 @@ CONFIGS = {
     "c2rmw": dict(program=lambda: prog_c2(rmw=True), pkt=64, n=16 * 1024 * 1024),
     "c3": dict(program=prog_c3, pkt="imix", n=16 * 1024 * 1024),
     "c3learn": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
+    "c3lru": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
     "c4": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024),
+    # C4 in AF_XDP frames: 2-KiB chunks, the packet after the 256-byte XDP headroom (xsk.go:695-701
+    # descriptors into a UMEM of fixed-size frames) instead of back to back
+    "c4f": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024, frame=(2048, 256)),
     "c5": dict(program=prog_c5, pkt=64, n=256 * 1024 * 1024),
     "bpf2bpf": dict(program=prog_bpf2bpf, pkt=64, n=4 * 1024 * 1024),
 }
@@ -526,6 +532,8 @@ def workload_maps(name: str) -> list[tuple[MapDef, tuple[np.ndarray, np.ndarray]
         return [(MapDef(MAP_ARRAY, 4, 8, 256), None)]
     if name in ("c3", "c3learn"):
         return [(MapDef(MAP_HASH, 16, 16, C3_MAX), c3_map_entries())]
+    if name == "c3lru":  # the learning flow table as an LRU_HASH (room for every flow: no eviction)
+        return [(MapDef(MAP_LRU_HASH, 16, 16, C3_MAX), c3_map_entries())]
     if name == "c5":
         return [(MapDef(MAP_HASH, 16, 16, C5_MAX), c5_map_entries())]
     if name == "bpf2bpf":
@@ -542,7 +550,7 @@ def headers(name: str, idx: np.ndarray, hdr: int = 64) -> np.ndarray:
         for b in range(hdr):
             h[:, b] = (r >> np.uint64(8 * (b % 8))) & np.uint64(0xFF)
         return h
-    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c4": headers_c4,
+    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c3lru": headers_c3learn, "c4": headers_c4, "c4f": headers_c4,
             "c5": headers_c5, "bpf2bpf": headers_bpf2bpf}[name](idx, hdr)
 
 
@@ -553,21 +561,33 @@ def packet_sizes(name: str, idx: np.ndarray) -> np.ndarray:
     return np.full(len(idx), int(p), dtype=np.int64)
 
 
+def packet_offsets(name: str, sizes: np.ndarray) -> tuple[np.ndarray, int]:
+    """UMEM address of every packet and the UMEM size: back to back (a compacted UMEM / pcap-style buffer),
+    or one fixed-size frame per packet after a headroom (configs with `frame`: an AF_XDP UMEM)."""
+    n = len(sizes)
+    frame = CONFIGS.get(name, {}).get("frame")
+    if frame:
+        chunk, head = frame
+        return np.arange(n, dtype=np.int64) * chunk + head, n * chunk
+    offs = np.zeros(n, dtype=np.int64)
+    if n:
+        offs[1:] = np.cumsum(sizes[:-1])
+    return offs, int(sizes.sum()) if n else 0
+
+
 def build_batch(name: str, start: int, n: int, hdr: int = 64):
     """Host batch for packets [start, start+n): (umem uint8, descs structured) with packets packed
-    back to back (a compacted AF_XDP UMEM / pcap-style buffer); bytes past `hdr` are zero."""
+    back to back (a compacted AF_XDP UMEM / pcap-style buffer) or in frames (packet_offsets); bytes past
+    `hdr` are zero."""
     from ._native import np_dtypes
     d_desc, _, _ = np_dtypes()
     idx = np.arange(start, start + n, dtype=np.uint64)
     sizes = packet_sizes(name, idx)
-    offs = np.zeros(n, dtype=np.int64)
-    if n:
-        offs[1:] = np.cumsum(sizes[:-1])
-    total = int(sizes.sum()) if n else 0
+    offs, total = packet_offsets(name, sizes)
     umem = np.zeros(max(total, 1), dtype=np.uint8)
     h = headers(name, idx, hdr)
     if n:
-        if np.all(sizes == sizes[0]) and sizes[0] >= hdr:
+        if np.all(sizes == sizes[0]) and sizes[0] >= hdr and not CONFIGS.get(name, {}).get("frame"):
             umem[:total].reshape(n, int(sizes[0]))[:, :hdr] = h
         else:
             cols = np.arange(hdr, dtype=np.int64)[None, :]

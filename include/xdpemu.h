@@ -75,6 +75,8 @@ extern "C" {
 #define XE_E_MAP_OP 16      /* map Lookup/Update/Push/Pop returned an error the helper does not map to
                              * errno, e.g. "update not available on this map type" (maps.go:61-82),
                              * "lookup didn't return a pointer" (helper_functions.go:178-181) */
+#define XE_E_HOST_HELPER 17 /* a host helper (xe_set_helper) returned an error: "helper function paniced"
+                             * (emulator/inst_call_helper.go:30-33); always with XE_E_IN_HELPER */
 #define XE_E_IN_HELPER 0x80
 
 /* PANIC codes (xe_result.code when status == XE_ST_PANIC) */
@@ -125,6 +127,7 @@ extern "C" {
 #define XE_MODE_PARALLEL 1   /* parallel only; conflicts reported in stats, results kept            */
 #define XE_MODE_SEQUENTIAL 2 /* exact packet order on one device lane                             */
 #define XE_MODE_KEYED 3      /* (xe_batch_stats.mode_used only) map-entry writes: per-key chains  */
+#define XE_MODE_CANCELLED 4  /* (xe_batch_stats.mode_used only) a pipelined batch xe_cancel dropped */
 
 /* AF_XDP descriptor, exactly the layout of gobpfld's xsk.go:695-701 */
 typedef struct xe_desc {
@@ -261,6 +264,13 @@ int xe_run_batch_device_async(xe_vm* vm, void* d_umem, uint64_t umem_len, const 
                               xe_batch_stats* stats);
 /* Complete every pipelined batch (replays included); returns the first error. */
 int xe_sync(xe_vm* vm);
+/* RunContext's cancellation (emulator/vm.go:117-134: ctx.Err() checked between steps) for the pipelined
+ * batches: every batch submitted with xe_run_batch_device_async whose stats are not filled yet is dropped.
+ * Batches still queued on the device exit at their first wave, the maps are put back to the state before
+ * the oldest dropped batch, and each dropped batch's stats get mode_used = XE_MODE_CANCELLED (its records
+ * and verdicts are undefined). The VM then holds exactly the effects of the batches that completed, in
+ * submission order. *cancelled (may be NULL) receives how many were dropped. */
+int xe_cancel(xe_vm* vm, uint32_t* cancelled);
 /* Build ahead of the next batch what it will run: map upload, engine choice and the per-program gfx950
  * kernel for the current program and map geometry (plus its keyed-execution variant when the program
  * may write map entries), so no batch pays a compile. Optional (the first batch does it otherwise); safe
@@ -358,6 +368,49 @@ int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len)
 int xe_compile_kernel_source(const char* src, const char* arch, const char* dir, char* err, size_t errlen);
 /* the file name (in the cache directory) of the code object a source compiles to for `arch` */
 int xe_kernel_object_name(const char* src, const char* arch, char* buf, size_t cap);
+
+/* --- Step / VM.String (emulator/vm.go:137-173, 248-270): per-packet instruction trace ---
+ * xe_trace_config selects packets by their index in each batch (at most XE_TRACE_MAX_PACKETS; duplicates
+ * collapse) and keeps the first max_steps steps of each (at most XE_TRACE_MAX_STEPS): after every
+ * instruction that completes (Step returns without an error; the exiting instruction included) one record
+ * of what VM.String prints — PC, PI, SF and R0..R10. While a trace is configured batches run on the
+ * interpreter engine and synchronously (pipelined batches too); a batch that is replayed in order or
+ * through the keyed path re-records what it re-runs, so the records are those of the execution whose
+ * results the batch reports. npk = 0 turns tracing off. */
+#define XE_TRACE_MAX_PACKETS 4096
+#define XE_TRACE_MAX_STEPS 65536
+typedef struct xe_trace_rec {
+    uint32_t packet;  /* index in the batch */
+    uint32_t step;    /* 0-based: the packet's step-th instruction */
+    int32_t pc;       /* PC of that instruction (Registers.PC before Step's increment) */
+    int32_t pi;       /* Registers.PI after it (a tail call changes it) */
+    uint32_t sf;      /* Registers.SF after it: bpf-to-bpf call depth */
+    uint8_t kind[11]; /* R0..R10: XE_KIND_* */
+    uint8_t pad;
+    int64_t val[11];  /* R0..R10: RegisterValue.Value() (a pointer's offset) */
+} xe_trace_rec;
+int xe_trace_config(xe_vm* vm, const uint32_t* packets, uint32_t npk, uint32_t max_steps);
+/* Records of packet `packet` of the last batch run (it must be one xe_trace_config named): out[0..*nsteps),
+ * *nsteps = min(steps the packet completed, max_steps); cap = room in out (NULL/0: query *nsteps). */
+int xe_trace_read(xe_vm* vm, uint32_t packet, xe_trace_rec* out, uint32_t cap, uint32_t* nsteps);
+
+/* --- the VM's helper table (VM.HelperFunctions, emulator/vm.go:23,35; HelperFunc,
+ * emulator/helper_functions.go:17) ---
+ * A host helper is called with R1..R5 (RegisterValue.Value() and XE_KIND_* of each: pointers pass their
+ * offset; the emulator's memory stays on the device) and the packet's index in the batch; it returns 0 and
+ * sets *r0, which becomes R0 (an IMM), or non-zero: the packet stops with XE_ST_VMERR, code
+ * XE_E_HOST_HELPER | XE_E_IN_HELPER ("helper function paniced", inst_call_helper.go:30-33). R1..R5 are
+ * left as they were (a HelperFunc "should never touch R6-R9" and the built-ins leave R1-R5 alone).
+ * Host helpers run in packet order on the exact one-lane path (the parallel pass defers a packet that
+ * calls one to it), on the host thread that called the batch, which serves the device's requests while
+ * the batch runs. */
+typedef int (*xe_helper_fn)(void* user, uint32_t packet, const int64_t args[5], const uint8_t kinds[5], int64_t* r0);
+/* id < 192 (LinuxHelperFunctions' table size). fn != NULL: the host function replaces table entry id
+ * (a built-in included); fn == NULL: the entry becomes nil (a call fails with XE_E_NO_HELPER,
+ * inst_call_helper.go:26-28). */
+int xe_set_helper(xe_vm* vm, uint32_t id, xe_helper_fn fn, void* user);
+/* entry id back to LinuxHelperFunctions' (emulator/helper_functions.go:20-44): the built-in or nil */
+int xe_reset_helper(xe_vm* vm, uint32_t id);
 
 /* --- debug hooks (no reference counterpart) ---
  * Permute the chunk -> wave schedule of the parallel passes (0 = the default walk; s > 0 = a fixed

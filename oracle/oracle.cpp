@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <list>
 #include <map>
 #include <memory>
 #include <string>
@@ -447,6 +448,16 @@ struct VM {
   std::vector<std::unique_ptr<Memory>> memArena;
   std::string lastError;
   uint64_t steps = 0;
+  // VM.HelperFunctions (vm.go:23,35): entries changed from LinuxHelperFunctions (helper_functions.go:20-44)
+  enum HelperEntry : uint8_t { H_BUILTIN = 0, H_HOST, H_NIL };
+  HelperEntry helper[192] = {};
+  xe_helper_fn helper_fn[192] = {};
+  void* helper_user[192] = {};
+  uint32_t packet = 0;  // the harness's packet index (passed to host helpers)
+  // Step records of the traced packets (orc_trace_config)
+  std::vector<uint32_t> trace_pk;
+  uint32_t trace_max = 0;
+  std::vector<std::vector<xe_trace_rec>> trace;
 
   template <class T, class... A> T* mk(A&&... a) {
     T* p = new T(std::forward<A>(a)...);
@@ -594,31 +605,34 @@ struct HashMap : Map {  // emulator/maps_hash.go; sha256(key) is unobservable, s
 
 // HashMapLRU, emulator/maps_hash_lru.go. Entries keyed by key bytes (sha256 is unobservable; a
 // ReadRange error gives the empty key, as `if !ok` ignores it, :76-79); UsageList holds keys, MRU first.
+// The UsageList slice is kept as a linked list plus an index of its elements: the same sequence after every
+// operation (keys are unique in it), with promote / delete in O(log n) instead of the slice's O(n) shifts,
+// so the oracle can replay bench-sized batches.
 struct LRUHashMap : Map {
   std::map<std::vector<uint8_t>, std::unique_ptr<ByteMemory>> values;
-  std::vector<std::vector<uint8_t>> usage;  // UsageList
+  std::list<std::vector<uint8_t>> usage;  // UsageList, index 0 first
+  std::map<std::vector<uint8_t>, std::list<std::vector<uint8_t>>::iterator> upos;  // its elements
   std::vector<std::unique_ptr<ByteMemory>> evicted;  // evicted values stay valid for pointers still held
+  void append(const std::vector<uint8_t>& key) {  // m.UsageList = append(m.UsageList, keyHash)
+    usage.push_back(key);
+    upos[key] = std::prev(usage.end());
+  }
   bool isHash() const override { return true; }
   std::vector<uint8_t> keyBytes(RV* key) {
     std::vector<uint8_t> k;
     if (readRangeRV(key, 0, def.key_size, &k) != 0) k.clear();
     return k;
   }
-  void promote(const std::vector<uint8_t>& key) {  // :51-68
-    size_t cur = 0;
-    for (size_t i = 0; i < usage.size(); i++)
-      if (usage[i] == key) { cur = i; break; }
-    if (cur == 0) return;
-    std::vector<uint8_t> k = usage[cur];
-    for (size_t i = cur; i > 0; i--) usage[i] = usage[i - 1];
-    usage[0] = k;
+  void promote(const std::vector<uint8_t>& key) {  // :51-68: not found or already first: nothing
+    auto p = upos.find(key);
+    if (p == upos.end() || p->second == usage.begin()) return;
+    usage.splice(usage.begin(), usage, p->second);  // the keys above it move one down, it goes first
   }
   void erase(const std::vector<uint8_t>& key) {  // delete, :163-183
-    size_t cur = usage.size();
-    for (size_t i = 0; i < usage.size(); i++)
-      if (usage[i] == key) { cur = i; break; }
-    if (cur == usage.size()) return;
-    usage.erase(usage.begin() + long(cur));
+    auto p = upos.find(key);
+    if (p == upos.end()) return;
+    usage.erase(p->second);
+    upos.erase(p);
     auto it = values.find(key);
     if (it != values.end()) { evicted.push_back(std::move(it->second)); values.erase(it); }
   }
@@ -647,7 +661,7 @@ struct LRUHashMap : Map {
       auto m = std::make_unique<ByteMemory>();
       m->region = XE_REGION_HASHVAL; m->mapidx = index;
       it = values.emplace(kb, std::move(m)).first;
-      usage.push_back(kb);
+      append(kb);
     }
     promote(kb);
     it->second->setBacking(std::move(vb));
@@ -802,6 +816,20 @@ static int tailCall(VM* vm) {
 }
 
 static int callHelper(VM* vm, int64_t id) {  // returns 0 or VM error code (already IN_HELPER-tagged)
+  if (id >= 0 && id < 192 && vm->helper[id] != VM::H_BUILTIN) {
+    if (vm->helper[id] == VM::H_NIL) return -1;  // f == nil: "VM has no helper function" (inst_call_helper.go:26-28)
+    // f(vm): a host function over R1..R5; an error aborts the run (inst_call_helper.go:30-33)
+    int64_t a[5];
+    uint8_t k[5];
+    for (int r = 0; r < 5; r++) {
+      a[r] = vm->R[r + 1] ? vm->R[r + 1]->Value() : 0;
+      k[r] = uint8_t(vm->R[r + 1] ? vm->R[r + 1]->kind() : XE_KIND_NIL);
+    }
+    int64_t r0 = 0;
+    if (vm->helper_fn[id](vm->helper_user[id], vm->packet, a, k, &r0)) return XE_E_HOST_HELPER | XE_E_IN_HELPER;
+    vm->R[0] = vm->newIMM(r0);
+    return 0;
+  }
   switch (id) {
     case 1: case 2: {  // MapLookupElement :46-73 / MapUpdateElement :76-101
       Map* m = nullptr;
@@ -1320,7 +1348,7 @@ int orc_map_update(orc_vm* o, int32_t mi, const void* key, const void* value) {
       auto bm = std::make_unique<ByteMemory>();
       bm->region = XE_REGION_HASHVAL; bm->mapidx = mi;
       it = l->values.emplace(k, std::move(bm)).first;
-      l->usage.push_back(k);
+      l->append(k);
     }
     l->promote(k);
     it->second->setBacking(std::vector<uint8_t>((const uint8_t*)value, (const uint8_t*)value + m->def.value_size));
@@ -1437,11 +1465,66 @@ int orc_map_lru_order(orc_vm* o, int32_t mi, void* keys, uint64_t cap, uint64_t*
   if (count) *count = l->usage.size();
   if (!keys) return XE_OK;
   if (cap < l->usage.size()) return XE_ERR_INVAL;
-  for (size_t i = 0; i < l->usage.size(); i++) {
-    uint8_t* kd = (uint8_t*)keys + i * l->def.key_size;
+  size_t i = 0;
+  for (const auto& k : l->usage) {
+    uint8_t* kd = (uint8_t*)keys + i++ * l->def.key_size;
     memset(kd, 0, l->def.key_size);
-    memcpy(kd, l->usage[i].data(), std::min<size_t>(l->usage[i].size(), l->def.key_size));
+    memcpy(kd, k.data(), std::min<size_t>(k.size(), l->def.key_size));
   }
+  return XE_OK;
+}
+
+// What VM.String prints after a Step (emulator/vm.go:248-270): PC, PI, SF, R0..R10
+static xe_trace_rec traceRec(VM& vm, uint32_t packet, uint32_t step, int64_t pc) {
+  xe_trace_rec r{};
+  r.packet = packet;
+  r.step = step;
+  r.pc = int32_t(pc);
+  r.pi = vm.PI;
+  r.sf = uint32_t(vm.preserved.size());
+  for (int k = 0; k < 10; k++) {
+    r.val[k] = vm.R[k] ? vm.R[k]->Value() : 0;
+    r.kind[k] = uint8_t(vm.R[k] ? vm.R[k]->kind() : XE_KIND_NIL);
+  }
+  r.val[10] = vm.R10 ? vm.R10->Value() : 0;
+  r.kind[10] = XE_KIND_FRAMEPTR;
+  return r;
+}
+
+int orc_trace_config(orc_vm* o, const uint32_t* packets, uint32_t npk, uint32_t max_steps) {
+  if (!o || (npk && !packets) || npk > XE_TRACE_MAX_PACKETS || max_steps > XE_TRACE_MAX_STEPS || (npk && !max_steps))
+    return XE_ERR_INVAL;
+  VM& vm = o->vm;
+  vm.trace_pk.assign(packets, packets + npk);
+  std::sort(vm.trace_pk.begin(), vm.trace_pk.end());
+  vm.trace_pk.erase(std::unique(vm.trace_pk.begin(), vm.trace_pk.end()), vm.trace_pk.end());
+  vm.trace_max = npk ? max_steps : 0;
+  vm.trace.assign(vm.trace_pk.size(), {});
+  return XE_OK;
+}
+
+int orc_trace_read(orc_vm* o, uint32_t packet, xe_trace_rec* out, uint32_t cap, uint32_t* nsteps) {
+  if (!o || !nsteps) return XE_ERR_INVAL;
+  VM& vm = o->vm;
+  auto it = std::lower_bound(vm.trace_pk.begin(), vm.trace_pk.end(), packet);
+  if (it == vm.trace_pk.end() || *it != packet) return XE_ERR_INVAL;
+  const auto& t = vm.trace[size_t(it - vm.trace_pk.begin())];
+  *nsteps = uint32_t(t.size());
+  if (out) memcpy(out, t.data(), std::min<size_t>(cap, t.size()) * sizeof(xe_trace_rec));
+  return XE_OK;
+}
+
+int orc_set_helper(orc_vm* o, uint32_t id, xe_helper_fn fn, void* user) {
+  if (!o || id >= 192) return XE_ERR_INVAL;
+  o->vm.helper[id] = fn ? VM::H_HOST : VM::H_NIL;
+  o->vm.helper_fn[id] = fn;
+  o->vm.helper_user[id] = user;
+  return XE_OK;
+}
+
+int orc_reset_helper(orc_vm* o, uint32_t id) {
+  if (!o || id >= 192) return XE_ERR_INVAL;
+  o->vm.helper[id] = VM::H_BUILTIN;
   return XE_OK;
 }
 
@@ -1452,8 +1535,15 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
                   xe_result* results, uint32_t* verdicts, xe_regs* regs, xe_batch_stats* stats) {
   VM& vm = o->vm;
   if (stats) memset(stats, 0, sizeof *stats);
+  for (auto& t : vm.trace) t.clear();
   for (uint32_t p = 0; p < n; p++) {
     reset(&vm);
+    vm.packet = p;
+    std::vector<xe_trace_rec>* tr = nullptr;  // this packet's Step records (orc_trace_config)
+    {
+      auto it = std::lower_bound(vm.trace_pk.begin(), vm.trace_pk.end(), p);
+      if (it != vm.trace_pk.end() && *it == p) tr = &vm.trace[size_t(it - vm.trace_pk.begin())];
+    }
     // Reset keeps PI (emulator/vm.go:211-246); a tail call in the previous packet would otherwise
     // start this one in another program: the harness re-applies SetEntrypoint per packet
     vm.PI = vm.entry;
@@ -1490,6 +1580,7 @@ int orc_run_batch(orc_vm* o, uint8_t* umem, uint64_t umem_len, const xe_desc* de
         int e = execute(&vm, prog[pc], &exit);
         res.pc = uint32_t(pc);
         if (e) { res.status = XE_ST_VMERR; res.code = uint16_t(e); break; }
+        if (tr && tr->size() < vm.trace_max) tr->push_back(traceRec(vm, p, uint32_t(tr->size()), pc));
         if (exit) break;
         if (int64_t(prog.size()) <= vm.PC + 1) {  // vm.go:162-167
           vm.PC = pc;

@@ -38,6 +38,13 @@ int orc_run_batch(orc_vm* vm, uint8_t* umem, uint64_t umem_len, const xe_desc* d
 /* decode + Go String() rendering of every instruction (one per line) */
 int orc_decode_text(const uint64_t* insns, uint32_t n, char* buf, size_t buflen);
 int orc_decode_names(const uint64_t* insns, uint32_t n, char* buf, size_t buflen);
+/* Step-by-step records (xe_trace_config / xe_trace_read semantics): after every Step that returns without
+ * an error, the registers as VM.String prints them (emulator/vm.go:137-173, 248-270) */
+int orc_trace_config(orc_vm* vm, const uint32_t* packets, uint32_t npk, uint32_t max_steps);
+int orc_trace_read(orc_vm* vm, uint32_t packet, xe_trace_rec* out, uint32_t cap, uint32_t* nsteps);
+/* VM.HelperFunctions entries (xe_set_helper / xe_reset_helper semantics) */
+int orc_set_helper(orc_vm* vm, uint32_t id, xe_helper_fn fn, void* user);
+int orc_reset_helper(orc_vm* vm, uint32_t id);
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,8 @@ def gpu_cases():
     import test_ordered_par as O
     for build, mdef, entries, _ in O.CASES.values():
         cases.append((build(), [mdef], entries, Settings()))
+    from gobpfld_amd import workloads as W
+    cases.append(lambda vm: W.setup_vm(vm, "c3lru"))
     import test_ref_examples as R
     for prog in (R.from_text(), R.from_literals()):
         cases.append((prog, [R.STATS_MAP], None, Settings(engine=JIT)))

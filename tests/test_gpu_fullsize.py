@@ -86,9 +86,9 @@ def _c5_truth(n):
 
 
 def test_c5_fullsize_per_flow_counters():
-    """C5's per-GPU shard of the bench (16M x 64 B here; the bench runs 32M per GPU): per-flow {pkts,
+    """C5's per-GPU shard of the bench (33,554,432 x 64 B, BASELINE configs[4] / 8): per-flow {pkts,
     bytes} equal the flow histogram of the generated stream, and a second run doubles them."""
-    n = N16M
+    n = 2 * N16M
     want_k, want_v = _c5_truth(n)
     ver, dumps, stats = _device_run("c5", n, runs=2)
     assert stats[0]["status_count"][0] == n and stats[0]["conflict"] == 0 and stats[0]["mode_used"] == MODE_PARALLEL
@@ -155,11 +155,12 @@ def test_c4_fullsize_first_match():
     assert (ver == want).all(), f"{int((ver != want).sum())} verdicts differ"
 
 
-def test_c3learn_keyed_bench_size_equals_oracle(oracle_lib):
-    """The bench's keyed side line (C3-learn, 4,194,304 IMIX packets whose misses insert their flow)
-    through the keyed path, against one sequential oracle VM: results, verdicts and the final table."""
+@pytest.mark.parametrize("n", [4 * 1024 * 1024, N16M], ids=["4M", "16M"])
+def test_c3learn_keyed_bench_size_equals_oracle(oracle_lib, n):
+    """The bench's keyed side line (C3-learn, 4,194,304 IMIX packets whose misses insert their flow) and
+    the 16M batch DESIGN.md quotes, through the keyed path, against one sequential oracle VM: results,
+    verdicts and the final table."""
     import torch
-    n = 4 * 1024 * 1024
     umem, descs = W.build_batch("c3learn", 0, n)
     ov = VM(Settings(), lib=oracle_lib)
     W.setup_vm(ov, "c3learn")

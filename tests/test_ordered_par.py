@@ -170,3 +170,48 @@ def test_perf_appends_device_two_batches(gpu_lib, oracle_lib):
     (gd, gm), (od, _) = outs
     assert gm == [MODE_PARALLEL, MODE_PARALLEL]
     assert len(gd) == len(od) and gd == od
+
+
+def _c3lru_run(lib, n, mode=None):
+    """C3-LRU (workloads: C3-learn over an LRU_HASH flow table) on one VM: results, verdicts, the table
+    and its UsageList."""
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd.emulator import VM, Settings
+    umem, descs = W.build_batch("c3lru", 0, n)
+    vm = VM(Settings() if mode is None else Settings(mode=mode), lib=lib)
+    W.setup_vm(vm, "c3lru")
+    r = vm.run_batch(umem, descs)
+    k, v = vm.map_dump(1)
+    usage = vm.map_lru_order(1)
+    vm.close()
+    return r, k, v, usage
+
+
+def _same_c3lru(a, b):
+    ra, ka, va, ua = a
+    rb, kb, vb, ub = b
+    bad = np.nonzero(ra.results != rb.results)[0]
+    assert len(bad) == 0, f"{len(bad)} results differ, first at {bad[0] if len(bad) else -1}"
+    assert (ra.verdicts == rb.verdicts).all()
+    assert np.array_equal(ka, kb) and np.array_equal(va, vb), "LRU flow table differs"
+    assert ua == ub, "UsageList differs"
+    assert ra.stats["steps"] == rb.stats["steps"]
+
+
+def test_c3lru_hostsim_keyed_equals_oracle(oracle_lib, hostsim_lib):
+    """An LRU flow table that learns (maps_hash_lru.go:93-161): the keyed path's result, UsageList
+    included, is the reference's packet-by-packet one."""
+    got = _c3lru_run(hostsim_lib, 20000)
+    _same_c3lru(got, _c3lru_run(oracle_lib, 20000))
+    assert got[0].stats["mode_used"] == MODE_KEYED
+    assert len(got[1]) > 65536  # it learned flows
+
+
+@pytest.mark.gpu
+def test_c3lru_device_keyed_equals_oracle(gpu_lib, oracle_lib):
+    """C3-LRU at the bench's keyed batch (4,194,304 IMIX packets, ~256K flows learned into a 1M-entry
+    LRU_HASH) through the keyed path against one sequential oracle VM: results, verdicts, table, UsageList."""
+    n = 4 * 1024 * 1024
+    got = _c3lru_run(gpu_lib, n)
+    assert got[0].stats["mode_used"] == MODE_KEYED, got[0].stats
+    _same_c3lru(got, _c3lru_run(oracle_lib, n))

@@ -326,6 +326,18 @@ struct XeTailArgs {
   XeTailMap tail[XE_TAIL_MAPS];
 };
 
+// List maps in a parallel run (XeParams::list): each QUEUE / STACK map's element count at the batch's
+// start, and per map the facts that decide afterwards whether the run equals packet order: sens = 1 + the
+// last packet whose list operation assumed no push happened before it in the batch, push = the first
+// packet that pushed (0xffffffff: none). Exact iff sens <= push for every map. popmask: maps popped.
+struct XeListRun {
+  uint32_t cnt0[64];
+  uint32_t sens[64];
+  uint32_t push[64];
+  unsigned long long popmask;
+  unsigned long long pad;
+};
+
 // per-launch parameters
 struct XeParams {
   const XeUop* prog;
@@ -375,6 +387,14 @@ struct XeParams {
   xe_trace_rec* trace;
   uint32_t* trace_cnt;
   uint32_t trace_npk, trace_max;
+  // QUEUE / STACK pops, peeks and lookups in a parallel run (xe_runtime.cpp, "list operations"): null
+  // list: off (such an operation raises XE_FLAG_ORDERED). pop_mode 1 = the count pass (a lane stops at
+  // its packet's first list operation, flagging popflag[i] = 1 for a pop), 2 = the pass in which the
+  // packet's pop takes the element at its rank popbase[i] among the batch's pops in packet order.
+  XeListRun* list;
+  uint32_t pop_mode;
+  uint32_t* popflag;
+  const uint32_t* popbase;
   // helper table (xe_set_helper): bit id of host[] = a host function, of nil[] = a nil entry
   uint64_t host_helpers[3];
   uint64_t nil_helpers[3];

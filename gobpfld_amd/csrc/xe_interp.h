@@ -86,6 +86,9 @@ XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
 XE_DEV unsigned long long xe_load_relaxed64(unsigned long long* p) {
   return __hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+XE_DEV void xe_atomic_max32(unsigned int* p, unsigned int v) {
+  __hip_atomic_fetch_max((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 XE_DEV uint64_t xe_lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
 XE_DEV uint32_t xe_shfl32(uint32_t v, int l) { return uint32_t(__shfl(int(v), l)); }
 #else
@@ -123,6 +126,10 @@ XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
   return o;
 }
 XE_DEV unsigned long long xe_load_relaxed64(unsigned long long* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+XE_DEV void xe_atomic_max32(unsigned int* p, unsigned int v) {
+  unsigned int o = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (o < v && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+}
 XE_DEV uint64_t xe_lanemask_lt() { return 0; }
 XE_DEV uint32_t xe_shfl32(uint32_t v, int) { return v; }
 #endif
@@ -293,6 +300,7 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #define XE_EV_CAP 0x3000
 #define XE_EV_ORD 0x4000
 #define XE_EV_EXIT 0x8000
+#define XE_EV_STOP 0x6000  // the count pass of parallel list operations: the lane's packet stops here
 #define XE_EV_CLASS(e) ((e) & 0xf000)
 #define XE_IS_PANIC(e) (XE_EV_CLASS(e) == XE_EV_PANIC)
 
@@ -400,6 +408,7 @@ struct XeLane {
   uint32_t npristine;     // private ByteMemories still reading through to their source
   uint32_t pidx;          // the packet's index in the batch (order key of its parallel appends)
   uint32_t oseq;          // appends the packet made so far
+  uint32_t npops;         // list pops the packet made so far (parallel list operations, P.list)
 #endif
   uint64_t odef;      // ids 1..6 still holding their ctx default
   // packet
@@ -899,6 +908,7 @@ XE_DEV uint64_t kid_slot(uint32_t m, const XeDevMap& M, uint32_t slot) {
 
 // D table (the keys some packet writes): open addressing over key ids, 0 = free
 XE_DEV int64_t dset_find(const XeKeyed& K, uint64_t kid) {
+  if (!kid) return -1;  // (key ids are never 0; 0 marks a free D slot)
   uint32_t idx = uint32_t(kid >> 4) & (K.dcap - 1);
 #pragma unroll 1
   for (uint32_t p = 0; p < K.dcap; p++) {
@@ -1795,6 +1805,34 @@ XE_DEV uint32_t list_at(const XeDevMap& M, uint64_t i) {  // Values[i] in Go sli
   const uint64_t head = *map_hdr(M, 0);
   return ((XE_GP(const uint32_t))M.link)[*map_hdr(M, 4) ? i : (head + i) % M.list_cap];
 }
+
+// ---- QUEUE / STACK operations in a parallel run (P.list; xe_runtime.cpp runs the passes).
+// In packet order, packet i's list operations see the batch's start contents minus the pops of the
+// packets before it (popbase[i], the count pass's prefix sum) and of its own earlier pops, plus the
+// pushes of the packets before it. Pushes only append (after the last element), so a queue position
+// inside the start contents does not depend on them; anything else (a queue position past them, any
+// stack position: pushes land on top) assumes no push came before and records the packet in sens, and
+// the host replays the batch in order when a push did (push[m] < sens[m]).
+XE_DEV bool list_par(const XeParams& P) { return P.list && P.mode == XE_MODE_PARALLEL; }
+XE_DEV uint64_t list_pops_before(const XeLane& L, const XeParams& P) {
+  return uint64_t(P.pop_mode == 2 ? P.popbase[L.pidx] : 0u) + L.npops;
+}
+XE_DEV void list_mark_sens(const XeLane& L, const XeParams& P, uint32_t m) { xe_atomic_max32(&P.list->sens[m], L.pidx + 1u); }
+// position (Go slice index) of Values[kv] for the lane's packet; false: out of range
+XE_DEV bool list_pos(const XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, int64_t kv, int64_t& pos) {
+  const int64_t q = int64_t(list_pops_before(L, P)), cnt0 = int64_t(P.list->cnt0[m]);
+  if (!*map_hdr(M, 4)) {  // queue: front = start position q
+    if (kv < 0) return false;
+    if (q + kv >= cnt0) { list_mark_sens(L, P, m); return false; }
+    pos = q + kv;
+    return true;
+  }
+  list_mark_sens(L, P, m);  // stack: Lookup(kv) counts from the top
+  const int64_t c = cnt0 - q;
+  if (kv < 0 || kv >= c) return false;
+  pos = c - 1 - kv;
+  return true;
+}
 #endif
 
 // ------------------------------------------------------------------ helpers
@@ -1888,7 +1926,11 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
   }
 #if XE_HAS_ORDERED
   if (M.kind == XE_DM_LIST || M.kind == XE_DM_PERF) {
-    if (xe_concurrent(P)) return XE_EV_ORD;  // the list changes in packet order
+    // the list changes in packet order: in parallel only through the list-run rules (list_par)
+    if (xe_concurrent(P) && !(M.kind == XE_DM_LIST && list_par(P))) return XE_EV_ORD;
+    // count pass: the packet's rank needs only its pops before here (none): it stops (a later pop of it
+    // finds no rank in the next pass and replays the batch in order)
+    if (xe_concurrent(P) && P.pop_mode == 1) return XE_EV_STOP;
     int64_t kv = 0;
     if (!peek) {
       int64_t off = XE_T_KIND(K.t) == XE_KIND_FRAMEPTR ? xe_wadd(XE_FRAME, K.v) : K.v;
@@ -1902,6 +1944,12 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
       if (kv >= cnt) return 0;
       if (kv < 0) return XE_EV_PANIC | XE_P_INDEX;
       out = XeReg{0, xe_h_make(XE_H_QVAL, m, uint32_t(kv)), XE_KIND_MEMPTR};
+      return 0;
+    }
+    if (xe_concurrent(P)) {  // Values[kv] in packet order: list_pos
+      int64_t pos;
+      if (!list_pos(L, P, m, M, kv, pos)) { err = -7; return 0; }  // errMapOutOfMemory
+      out = XeReg{0, xe_h_make(XE_H_QVAL, m, list_at(M, uint64_t(pos))), XE_KIND_MEMPTR};
       return 0;
     }
     const int64_t cnt = int64_t(*map_hdr(M, 1));
@@ -2141,6 +2189,7 @@ XE_COLD int list_push_par(XeLane& L, const XeParams& P, uint32_t m, const XeDevM
   err = 0;
   if (!XE_ISPTR(R.t)) { err = -14; return 0; }
   if (L.oseq >= 0xffffu) return XE_EV_ORD;  // the tag's append number is 16 bits
+  if (P.list && M.kind == XE_DM_LIST) xe_atomic_min32(&P.list->push[m], L.pidx);  // (list_pos)
   const uint64_t tag = (uint64_t(L.pidx) << 16) | L.oseq++;
   if (M.kind == XE_DM_PERF) {
     int ve = ptr_read_range(L, P, R, size, [&](int64_t, uint8_t) {});
@@ -2294,10 +2343,20 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       reg_replace(L, 0, XE_KIND_IMM, 0, 0, 0);
       const XeDevMap M = map_desc(L, m);
       if (M.kind != XE_DM_LIST) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "pop not available"
-      if (xe_concurrent(P)) return XE_EV_ORD;
       XeReg val{0, 0, XE_KIND_IMM};
-      const uint64_t cnt = *map_hdr(M, 1);
-      if (cnt) {
+      if (xe_concurrent(P)) {
+        // the count pass flags the packet and stops it; the next pass pops the element at the packet's
+        // rank (one pop per packet: a second one replays the batch in order)
+        if (!list_par(P) || P.pop_mode == 0 || L.npops || (P.pop_mode == 2 && !P.popflag[L.pidx])) return XE_EV_ORD;
+        if (P.pop_mode == 1) {
+          P.popflag[L.pidx] = 1u;
+          xe_atomic_or64(&P.list->popmask, 1ull << m);
+          return XE_EV_STOP;
+        }
+        int64_t pos;
+        if (list_pos(L, P, m, M, 0, pos)) val = XeReg{0, xe_h_make(XE_H_QVAL, m, list_at(M, uint64_t(pos))), XE_KIND_MEMPTR};
+        L.npops++;
+      } else if (const uint64_t cnt = *map_hdr(M, 1)) {
         uint32_t id;
         if (*map_hdr(M, 4)) {
           id = list_at(M, cnt - 1);
@@ -2911,6 +2970,7 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   L.ctxdirty = 0;
   L.npres = 0;  // the harness sets PreservedRegisters = nil
   L.pi = P.entry;
+  L.npops = 0;
   L.npristine = 0;
 #endif
   L.odef = 0x7eull;
@@ -3116,17 +3176,20 @@ XE_DEV void keyed_dset_item(const XeKeyed& K, uint32_t i) {
   }
 }
 XE_DEV uint32_t keyed_root(const XeKeyed& K, uint32_t x) {
+  // parents only decrease (keyed_union_item hooks under the smaller root), so the walk ends
 #pragma unroll 1
-  for (;;) {
+  for (uint32_t hop = 0; hop < K.dcap; hop++) {
     const uint32_t p = xe_load_relaxed32(K.dcomp + x);
-    if (p == x) return x;
+    if (p == x || p >= K.dcap) return x;
     x = p;
   }
+  return x;
 }
 // hook every root of packet i's D keys under the smallest (parents only decrease: rounds converge)
 XE_DEV void keyed_union_item(const XeKeyed& K, uint32_t i) {
-  const uint32_t n = K.kcnt[i] < XE_KLOG ? K.kcnt[i] : XE_KLOG;
-  if (n < 2) return;
+  // an overflowed log (kcnt > XE_KLOG: the batch takes the replay) may hold entries never written
+  const uint32_t n = K.kcnt[i];
+  if (n < 2 || n > XE_KLOG) return;
   uint32_t r = XE_NONE;
 #pragma unroll 1
   for (uint32_t j = 0; j < n; j++) {
@@ -3146,7 +3209,7 @@ XE_DEV void keyed_compress_item(const XeKeyed& K, uint32_t x) {
   if (((XE_GP(const unsigned long long))K.dkid)[x]) K.dcomp[x] = keyed_root(K, x);
 }
 XE_DEV void keyed_assign_item(const XeKeyed& K, uint32_t i, uint8_t* skip) {
-  const uint32_t n = K.kcnt[i] < XE_KLOG ? K.kcnt[i] : XE_KLOG;
+  const uint32_t n = K.kcnt[i] <= XE_KLOG ? K.kcnt[i] : 0u;  // (overflow: see keyed_union_item)
   uint32_t c = K.dcap;
   int64_t d[XE_KLOG];
 #pragma unroll
@@ -3312,6 +3375,7 @@ XE_DEV void chain_packets(XeLane& L, const XeParams& P, uint32_t g, uint32_t nth
 XE_DEV void status_from_error(int e, int& status, int& code) {
   if (e == XE_EV_EXIT) { status = XE_ST_OK; }
   else if (XE_EV_CLASS(e) == XE_EV_ORD) { status = XE_ST_INTERNAL_ORDERED; }
+  else if (e == XE_EV_STOP) { status = XE_ST_OK; }  // (the count pass's records are discarded)
   else if (XE_EV_CLASS(e) == XE_EV_CAP) { status = XE_ST_INTERNAL_CAPACITY; }
   else if (XE_EV_CLASS(e) == XE_EV_UNSUP) { status = XE_ST_UNSUPPORTED; }
   else if (XE_IS_PANIC(e)) { status = XE_ST_PANIC; code = e & 0xff; }

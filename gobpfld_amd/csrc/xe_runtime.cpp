@@ -62,7 +62,16 @@ namespace {
 
 // ------------------------------------------------------------------ backend
 #ifdef XE_HOSTSIM
+#ifdef XE_HOSTSIM_POISON  // (sanitizer build) device memory starts as garbage, as hipMalloc's may
+int dev_alloc(void** p, size_t n) {
+  n = n ? n : 8;
+  *p = malloc(n);
+  if (*p) memset(*p, 0xA5, n);
+  return *p ? 0 : -1;
+}
+#else
 int dev_alloc(void** p, size_t n) { *p = calloc(n ? n : 8, 1); return *p ? 0 : -1; }
+#endif
 void dev_free(void* p) { free(p); }
 int h2d(void* d, const void* h, size_t n, xe_stream_t) { memcpy(d, h, n); return 0; }
 int d2h(void* h, const void* d, size_t n, xe_stream_t) { memcpy(h, d, n); return 0; }
@@ -71,6 +80,9 @@ int dmemset(void* d, int v, size_t n, xe_stream_t) { memset(d, v, n); return 0; 
 int dsync(xe_stream_t) { return 0; }
 int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   XeLane L;
+#ifdef XE_HOSTSIM_POISON  // registers a kernel never wrote: zero, the value a fresh VGPR often holds
+  memset(static_cast<void*>(&L), 0, sizeof L);
+#endif
   static thread_local uint8_t hdrbuf[XE_HDR_WAVE_BYTES + 16];  // one per host thread (xe_multi runs shards concurrently)
   L.hdrbuf = hdrbuf;
   XePend pend;
@@ -823,6 +835,12 @@ struct xe_vm {
   // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
   // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
   uint32_t keyed_backoff = 0;
+  // parallel list operations (XeListRun): the run's record, the count pass's per-packet flags and their
+  // prefix sum (pop ranks)
+  XeListRun* d_listrun = nullptr;
+  uint32_t* d_popflag = nullptr;
+  uint32_t* d_popbase = nullptr;
+  size_t pop_n = 0;
   // instruction trace (xe_trace_config): the traced packets (sorted), records kept per packet, device
   // copies (records, per-packet counts)
   std::vector<uint32_t> trace_pk;
@@ -1399,6 +1417,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_poison);
   stream_destroy(vm->cancel_stream);
   dev_free(vm->d_trace_pk); dev_free(vm->d_trace); dev_free(vm->d_trace_cnt);
+  dev_free(vm->d_listrun); dev_free(vm->d_popflag); dev_free(vm->d_popbase);
   host_free(vm->h_hostcall);
   for (auto& m : vm->maps) map_free_device(m);
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
@@ -1833,16 +1852,29 @@ static bool has_callbpf(const xe_vm* vm) {
   return false;
 }
 // The ordered maps a parallel run can serve: QUEUE / STACK pushes and PERF outputs (appends, put in
-// packet order after the run) and LRU_HASH lookups (promotions, applied by last touch after the run);
-// any other operation on them (pops, peeks, list / event lookups, LRU updates and deletes) raises
-// XE_FLAG_ORDERED and the batch replays in packet order.
+// packet order after the run), LRU_HASH lookups (promotions, applied by last touch after the run),
+// LRU_HASH updates (keyed chains), and QUEUE / STACK pops, peeks and lookups (list_ops: a count pass
+// ranks the pops in packet order). What remains raises XE_FLAG_ORDERED and the batch replays in packet
+// order: PERF event lookups, LRU deletes and evictions, a second pop in one packet, a list position that
+// depends on a push made earlier in the batch.
 static bool ordered_parallel_ok(const xe_vm* vm) {
-  // a static screen: pops and peeks (helpers 88 / 89) take the list's head in packet order, so a VM whose
-  // programs can call them skips the parallel try (and its rollback) and replays in order straight away
+  // a static screen: indirect helper calls are not analysed (a pop behind one would find no count pass)
   for (size_t p = 1; p < vm->programs.size(); p++)
     for (const XeUop& u : vm->programs[p])
-      if (u.cls == U_HELPER && (u.imm == 88 || u.imm == 89)) return false;
+      if (u.cls == U_CALLX) return false;
   return true;
+}
+// the VM's programs may pop a QUEUE / STACK (the parallel run then starts with the count pass)
+static bool may_pop(const xe_vm* vm) {
+  for (size_t p = 1; p < vm->programs.size(); p++)
+    for (const XeUop& u : vm->programs[p])
+      if (u.cls == U_HELPER && u.imm == 88) return true;
+  return false;
+}
+static bool has_list_maps(const xe_vm* vm) {
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].dkind == XE_DM_LIST) return true;
+  return false;
 }
 // the ordered maps' header words (counts, next ids, event bytes) at the start of a parallel run, and
 // the LRU maps' value pools (a parallel run adds into looked-up values in place)
@@ -2565,8 +2597,35 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     vm->last_grid = parallel_grid(vm, pj, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     uint32_t flags = 0;
-    for (int attempt = 0;; attempt++) {
-      if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
+    // QUEUE / STACK pops, peeks and lookups in parallel (xe_interp.h list_pos): the run's list record,
+    // and for a program that may pop, a count pass first (which packets pop: their prefix sum is each
+    // pop's rank in packet order), then the pass proper from the batch's start again
+    const bool lists = ordmaps && n > 0 && has_list_maps(vm);
+    const bool pops = lists && may_pop(vm);
+    bool list_conflict = false;
+    uint32_t pop_map = 0;
+    if (lists) {
+      if (!vm->d_listrun && dev_alloc((void**)&vm->d_listrun, sizeof(XeListRun))) return fail(vm, XE_ERR_NOMEM, "device alloc (lists)");
+      P.list = vm->d_listrun;
+      if (pops && vm->pop_n < n) {
+        dev_free(vm->d_popflag); dev_free(vm->d_popbase);
+        vm->d_popflag = vm->d_popbase = nullptr;
+        vm->pop_n = 0;
+        if (dev_alloc((void**)&vm->d_popflag, size_t(n) * 4) || dev_alloc((void**)&vm->d_popbase, size_t(n) * 4))
+          return fail(vm, XE_ERR_NOMEM, "device alloc (pop ranks)");
+        vm->pop_n = n;
+      }
+    }
+    XeListRun lr{};
+    auto list_init = [&]() -> int {  // start counts from the headers, no sensitive op, no push yet
+      memset(&lr, 0, sizeof lr);
+      for (size_t i = 1; i < vm->maps.size() && i < 64; i++)
+        if (vm->maps[i].dkind == XE_DM_LIST) lr.cnt0[i] = uint32_t(ord_h0[i * 8 + 1]);
+      for (int i = 0; i < 64; i++) lr.push[i] = 0xffffffffu;
+      return h2d(vm->d_listrun, &lr, sizeof lr, s);
+    };
+    auto list_read = [&]() -> int { return d2h(&lr, vm->d_listrun, sizeof lr, s) || dsync(s); };
+    auto pass = [&]() -> int {
       if (pj ? launch_jit(pj, &P, vm->last_grid, 256, s) : launch_interp(&P, vm->last_grid, 256, s))
         return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t1.rec(s);  // kernel_ms: the emulator kernel alone
@@ -2575,6 +2634,49 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       kms = Timer::ms(vm->t0, vm->t1);
       flags = uint32_t(red[0]);
       conflict = run_conflict(red, P.nmaps);
+      return XE_OK;
+    };
+    for (int attempt = 0;; attempt++) {
+      if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
+      if (lists && list_init()) return fail(vm, XE_ERR_DEVICE, "list run");
+      if (pops) {
+        P.pop_mode = 1;
+        P.popflag = vm->d_popflag;
+        P.popbase = nullptr;
+        if (dmemset(vm->d_popflag, 0, size_t(n) * 4, s)) return fail(vm, XE_ERR_DEVICE, "pop flags");
+        if (int rc = pass()) return rc;
+        if (!conflict) {
+          if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
+          if (lr.popmask & (lr.popmask - 1)) {  // pops from more than one list: one rank order per map is not kept
+            list_conflict = conflict = true;
+            flags |= XE_FLAG_ORDERED;
+          } else {
+            pop_map = lr.popmask ? uint32_t(__builtin_ctzll(lr.popmask)) : 0u;
+            XeKeyed S{};
+            S.iota = vm->d_popflag;
+            S.ckey = vm->d_popbase;
+            size_t sb = 0;
+            if (rollback(false) || ordered_hdr_restore(vm, ord_h0, s) || list_init() ||
+                launch_keyed_scan(&S, n, nullptr, &sb, s) || ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb) ||
+                launch_keyed_scan(&S, n, vm->d_ksort, &sb, s))
+              return fail(vm, XE_ERR_DEVICE, "pop ranks");
+            P.pop_mode = 2;
+            P.popbase = vm->d_popbase;
+            if (int rc = pass()) return rc;
+          }
+        }
+      } else if (int rc = pass()) {
+        return rc;
+      }
+      if (!conflict && lists) {  // exact only if no list position depended on an earlier push
+        if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
+        for (int i = 0; i < 64; i++)
+          if (lr.sens[i] > lr.push[i]) list_conflict = true;
+        if (list_conflict) {
+          conflict = true;
+          flags |= XE_FLAG_ORDERED;
+        }
+      }
       // appends past an ordered map's device room: the atomics counted every attempted append, so the
       // room grows to what the batch needs and the parallel pass runs once more
       if (ordmaps && attempt == 0 && (flags & XE_FLAG_CAPACITY) && !(flags & XE_FLAG_ORDERED)) {
@@ -2595,7 +2697,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (ordmaps)  // the appends of the run are past the restored counts: unreferenced
         if (ordered_hdr_restore(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "rollback (ordered maps)");
       int r = 1;
-      const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY);
+      const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY) && !list_conflict;
       if (try_keyed && vm->keyed_backoff) vm->keyed_backoff--;
       else if (try_keyed) {
         vm->t2.rec(s);
@@ -2617,8 +2719,28 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       }
     } else if (!conflict) {
       vm->keyed_backoff = 0;
-      // the run's results stand: its appends into packet order
-      if (ordmaps && ordered_finalize(vm, ord_h0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
+      // the run's results stand: its appends into packet order, then its pops off the popped list (a
+      // stack's pushes all came after its pops, so they land on the lowered top)
+      if (ordmaps) {
+        std::vector<uint64_t> h0 = ord_h0;
+        uint64_t k = 0;
+        if (pop_map) {
+          uint32_t last[2] = {0, 0};
+          if (d2h(&last[0], vm->d_popflag + (n - 1), 4, s) || d2h(&last[1], vm->d_popbase + (n - 1), 4, s) || dsync(s))
+            return fail(vm, XE_ERR_DEVICE, "pop count");
+          k = std::min<uint64_t>(uint64_t(last[0]) + last[1], ord_h0[pop_map * 8 + 1]);
+          if (vm->maps[pop_map].stack) h0[pop_map * 8 + 1] -= k;
+        }
+        if (ordered_finalize(vm, h0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
+        if (k) {
+          HostMap& m = vm->maps[pop_map];
+          uint64_t hdr[8];
+          if (d2h(hdr, m.d_hdr, 64, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "pops");
+          if (!m.stack) hdr[0] = (hdr[0] + k) % m.list_cap;
+          hdr[1] -= k;
+          if (h2d(m.d_hdr, hdr, 64, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "pops");
+        }
+      }
     }
   }
   vm->keyed_hint = used == XE_MODE_KEYED;

@@ -95,6 +95,61 @@ def prog_lru_queue():
     return a.assemble()
 
 
+def prog_consume(push=True, peek=None, two_pops=False):
+    """A work queue: when packet[9] is even pop one element (the count pass ranks the pops in packet
+    order); a popped element's value (or 7 when the list was empty) goes into R8 and the verdict; push:
+    then push packet[0:8]; peek "first" / "after": peek at the front (helper 89) before the pop (the
+    count pass then cannot rank the pops: in order) or after it, and add the value; two_pops: pop twice
+    (the second pop replays the batch in order)."""
+    a = Asm()
+    _head(a, 16)
+    a.mov64(8, 7)
+
+    def do_peek(tag):
+        a.ld_map(1, 1).mov64(2, src=10).add64(2, -32).call(89)
+        a.jmp(JNE, 0, "nopeek" + tag, imm=0)
+        a.ldx(8, 5, 2, 0).alu64(0x00, 8, src=5)
+        a.label("nopeek" + tag)
+
+    if peek == "first":
+        do_peek("0")
+    a.ldx(1, 4, 6, 9).alu64(0x50, 4, 1).jmp(JNE, 4, "nopop", imm=0)
+    for k in range(2 if two_pops else 1):
+        a.ld_map(1, 1).mov64(2, src=10).add64(2, -24).call(88)
+    a.ldx(8, 3, 10, -24)
+    a.jmp(JEQ, 3, "nopop", imm=0)                # IMM 0: the list was empty (a pointer never equals 0)
+    a.ldx(8, 4, 3, 0).alu64(0x00, 8, src=4)      # r8 += element value
+    a.label("nopop")
+    if peek == "after":
+        do_peek("1")
+    if push:
+        a.ldx(8, 3, 6, 0).stx(8, 10, -8, 3)
+        a.ld_map(1, 1).mov64(2, src=10).add64(2, -8).mov64(3, 0).call(87)
+    a.label("out").mov64(0, src=8).alu64(0x50, 0, 3).exit()   # verdict = r8 & 3
+    return a.assemble()
+
+
+def prog_peek():
+    """Reads only: peek at the front and look up element packet[1] % 64 by index (helper 1 on a queue);
+    then push packet[0:8] — the reads sit inside the start contents, so the pushes do not move them."""
+    a = Asm()
+    _head(a, 16)
+    a.mov64(8, 0)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -32).call(89)
+    a.jmp(JNE, 0, "nopeek", imm=0)
+    a.ldx(8, 8, 2, 0)
+    a.label("nopeek")
+    a.ldx(1, 3, 6, 1).alu64(0x50, 3, 63).stx(4, 10, -4, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4).call(1)
+    a.jmp(JEQ, 0, "push", imm=0)
+    a.ldx(8, 4, 0, 0).alu64(0x00, 8, src=4)
+    a.label("push")
+    a.ldx(8, 3, 6, 0).stx(8, 10, -16, 3)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -16).mov64(3, 0).call(87)
+    a.label("out").mov64(0, src=8).alu64(0x50, 0, 3).exit()
+    return a.assemble()
+
+
 LRU = (MapDef(MAP_LRU_HASH, 4, 8, 64), None)
 LRU_ROOMY = (MapDef(MAP_LRU_HASH, 4, 8, 128), None)  # every key of the stream fits: no eviction
 LRU_PRELOAD = {0: [(k.to_bytes(4, "little"), (1000 * k).to_bytes(8, "little")) for k in range(0, 96, 2)]}
@@ -103,6 +158,10 @@ STACK = (MapDef(MAP_STACK, 0, 8, 16), None)
 PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
 PRELOAD = {0: [(None, (0xAB00 + i).to_bytes(8, "little")) for i in range(3)]}  # userspace pushes first
 QUEUE_BIG = (MapDef(MAP_QUEUE, 0, 8, 1 << 20), None)
+LISTQ = (MapDef(MAP_QUEUE, 0, 8, 8192), None)
+LISTS = (MapDef(MAP_STACK, 0, 8, 8192), None)
+LIST_PRELOAD = {0: [(None, (0xC000 + i).to_bytes(8, "little")) for i in range(1536)]}  # more than the pops
+LIST_SHORT = {0: [(None, (0xC000 + i).to_bytes(8, "little")) for i in range(40)]}    # fewer than the pops
 
 CASES = {
     "queue": (prog_push, QUEUE, PRELOAD, MODE_PARALLEL),
@@ -114,6 +173,19 @@ CASES = {
     # LRU learning without eviction: the keyed path (misses insert, later packets of the key hit it)
     "lru_learn": (lambda: prog_lru(update=True), LRU_ROOMY, LRU_PRELOAD, MODE_KEYED),
     "lru_learn_queue": (prog_lru_queue, LRU_ROOMY, LRU_PRELOAD, MODE_KEYED),
+    # pops / peeks in parallel (xe_interp.h list_pos): the count pass ranks each packet's pop
+    "queue_consume": (prog_consume, LISTQ, LIST_PRELOAD, MODE_PARALLEL),
+    "queue_consume_peek": (lambda: prog_consume(peek="after"), LISTQ, LIST_PRELOAD, MODE_PARALLEL),
+    "stack_consume_peek": (lambda: prog_consume(peek="after", push=False), LISTS, LIST_PRELOAD, MODE_PARALLEL),
+    "queue_peek_then_pop": (lambda: prog_consume(peek="first"), LISTQ, LIST_PRELOAD, MODE_SEQUENTIAL),
+    "stack_consume": (lambda: prog_consume(push=False), LISTS, LIST_PRELOAD, MODE_PARALLEL),
+    "queue_drained_no_push": (lambda: prog_consume(push=False), LISTQ, LIST_SHORT, MODE_PARALLEL),
+    # ... and what must still replay in order: a pop past the start contents after an earlier push, a
+    # stack pop after a push, two pops in one packet
+    "queue_drained_push": (prog_consume, LISTQ, LIST_SHORT, MODE_SEQUENTIAL),
+    "stack_consume_push": (prog_consume, LISTS, LIST_PRELOAD, MODE_SEQUENTIAL),
+    "queue_two_pops": (lambda: prog_consume(two_pops=True), LISTQ, LIST_PRELOAD, MODE_SEQUENTIAL),
+    "queue_peek_only": (prog_peek, LISTQ, LIST_PRELOAD, MODE_PARALLEL),
 }
 
 

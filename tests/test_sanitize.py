@@ -1,7 +1,10 @@
 """ASan/UBSan builds of the oracle and of the host simulation of the device logic: both are
 compiled with -fsanitize=address,undefined (no recovery), a sanitized C++ driver runs every KAT, a
 slice of the differential fuzzer and the BASELINE configs at small sizes through both and compares
-every observable (tests/sanitize/san_driver.cpp). A sanitizer report fails the test."""
+every observable (tests/sanitize/san_driver.cpp). A sanitizer report fails the test. The host simulation is
+built with XE_HOSTSIM_POISON: device allocations start as 0xA5 garbage (hipMalloc does not clear) and the
+simulated lane's registers as zero, so logic that reads what it never wrote shows up here rather than as a
+device fault that depends on what an earlier kernel left in memory."""
 import os
 import shutil
 import subprocess
@@ -38,7 +41,7 @@ def test_sanitized_oracle_and_hostsim_agree(tmp_path):
                  [ROOT / "oracle" / "oracle.cpp", ROOT / "oracle" / "oracle.h", *hdrs])
     sim_src = [csrc / "xe_runtime.cpp", csrc / "xe_io.cpp", csrc / "xe_multi.cpp", csrc / "xe_jit.cpp"]
     sim = _build(OUT / "libxdpemu_hostsim_san.so",
-                 [cxx, *FLAGS, "-fPIC", "-shared", "-DXE_HOSTSIM", *map(str, sim_src), "-pthread"], sim_src + hdrs)
+                 [cxx, *FLAGS, "-fPIC", "-shared", "-DXE_HOSTSIM", "-DXE_HOSTSIM_POISON", *map(str, sim_src), "-pthread"], sim_src + hdrs)
     drv = _build(OUT / "san_driver", [cxx, *FLAGS, str(SAN / "san_driver.cpp"), "-ldl"], [SAN / "san_driver.cpp"])
     import importlib.util
     spec = importlib.util.spec_from_file_location("san_cases", SAN / "cases.py")

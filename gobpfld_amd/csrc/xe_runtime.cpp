@@ -1975,7 +1975,8 @@ static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t
 // room for twice what the pass tried to append. 1: grown, 0: no ordered map was short, < 0: error.
 static int ordered_grow(xe_vm* vm, const std::vector<uint64_t>& h0, xe_stream_t s) {
   std::vector<uint64_t> h1;
-  if (ordered_hdr_read(vm, h1, s)) return -1;
+  // the header words only: the LRU pools' snapshot is the pass's start, which the restore below needs
+  if (ordered_hdr_read(vm, h1, s, false)) return -1;
   bool short_room = false;
   uint64_t slack = vm->ord_slack, bytes = vm->ord_slack_bytes;
   for (size_t i = 1; i < vm->maps.size(); i++) {
@@ -2437,6 +2438,17 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (klaunch(&X, grid) || fold()) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed spec)");
     if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed spec)");
     uint32_t flags = uint32_t(red[0]);
+    if (ordmaps && (flags & XE_FLAG_CAPACITY) && !(flags & XE_FLAG_ORDERED)) {
+      // appends past an ordered map's device room (the parallel branch's ordered_grow): the room
+      // grows to what the pass tried to append and the keyed path starts over
+      const int g = ordered_grow(vm, kh0, s);
+      if (g < 0) return fail(vm, XE_ERR_DEVICE, "ordered map room");
+      if (g == 1) {
+        if (rollback(false) || prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+        P.maps = vm->d_maps;
+        return 2;
+      }
+    }
     if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) return krollback() ? -1 : 1;
     if (!(flags & XE_FLAG_KEYED)) {  // no packet wrote a map entry: an ordinary parallel run
       if (run_conflict(red, P.nmaps)) return krollback() ? -1 : 1;

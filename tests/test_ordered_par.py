@@ -158,9 +158,9 @@ STACK = (MapDef(MAP_STACK, 0, 8, 16), None)
 PERF = (MapDef(MAP_PERF_EVENT_ARRAY, 4, 4, 8), None)
 PRELOAD = {0: [(None, (0xAB00 + i).to_bytes(8, "little")) for i in range(3)]}  # userspace pushes first
 QUEUE_BIG = (MapDef(MAP_QUEUE, 0, 8, 1 << 20), None)
-LISTQ = (MapDef(MAP_QUEUE, 0, 8, 8192), None)
-LISTS = (MapDef(MAP_STACK, 0, 8, 8192), None)
-LIST_PRELOAD = {0: [(None, (0xC000 + i).to_bytes(8, "little")) for i in range(1536)]}  # more than the pops
+LISTQ = (MapDef(MAP_QUEUE, 0, 8, 16384), None)
+LISTS = (MapDef(MAP_STACK, 0, 8, 16384), None)
+LIST_PRELOAD = {0: [(None, (0xC000 + i).to_bytes(8, "little")) for i in range(3072)]}  # more than the pops
 LIST_SHORT = {0: [(None, (0xC000 + i).to_bytes(8, "little")) for i in range(40)]}    # fewer than the pops
 
 CASES = {
@@ -203,20 +203,22 @@ def test_appends_hostsim_equal_oracle(oracle_lib, hostsim_lib, name):
     assert got[0].stats["mode_used"] == CASES[name][3]
 
 
-@pytest.mark.parametrize("name", ["queue", "perf"])
+@pytest.mark.parametrize("name", ["queue", "perf", "lru_learn_queue"])
 def test_appends_hostsim_past_device_room(oracle_lib, hostsim_lib, name):
     """More appends than the device room a run starts with (xe_runtime.cpp ord_slack, 4096 elements /
-    events): the parallel pass counts every attempted append, ordered_grow resizes the device lists and
-    the pass runs once more — still PARALLEL, still the reference's list."""
+    events): the pass counts every attempted append, ordered_grow resizes the device lists and the pass
+    (the parallel one, or the keyed path's SPEC pass) runs once more — still the reference's list, still
+    the case's mode."""
     got = _run(hostsim_lib, name, 6144)
     assert_same(got, _run(oracle_lib, name, 6144), name)
-    assert got[0].stats["mode_used"] == MODE_PARALLEL
+    assert got[0].stats["mode_used"] == CASES[name][3]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_appends_device_equal_oracle(gpu_lib, oracle_lib, name):
-    n = 4096 if name in ("queue_pop", "lru_update") else 262144
+    # the list cases pop about every other packet: 4096 packets stay inside their 3072 preloaded elements
+    n = 4096 if name in ("queue_pop", "lru_update") or CASES[name][1] in (LISTQ, LISTS) else 262144
     got = _run(gpu_lib, name, n)
     assert_same(got, _run(oracle_lib, name, n), name)
     assert got[0].stats["mode_used"] == CASES[name][3]

@@ -356,6 +356,8 @@ XE_DEV uint64_t xe_ctx_default_word(int w) {
 #ifndef XE_ACC
 #define XE_ACC 64
 #endif
+// log2(XE_ACC): acc_slot takes that many top bits of its hash (64..1024 entries)
+#define XE_ACC_BITS (XE_ACC >= 1024 ? 10 : XE_ACC >= 512 ? 9 : XE_ACC >= 256 ? 8 : XE_ACC >= 128 ? 7 : 6)
 struct XeAcc {
   unsigned long long tag[XE_ACC];
   unsigned long long sum[XE_ACC];
@@ -1246,7 +1248,7 @@ XE_DEV int xe_lds_add32(int* p, int v) { int o = *p; *p += v; return o; }
 #endif
 
 XE_DEV uint32_t acc_slot(uint64_t addr) {
-  return uint32_t(((addr >> 2) * 0x9E3779B97F4A7C15ull) >> 58) & (XE_ACC - 1);
+  return uint32_t(((addr >> 2) * 0x9E3779B97F4A7C15ull) >> (64 - XE_ACC_BITS)) & (XE_ACC - 1);
 }
 
 // One HBM add of a (deferred) sum into an aligned 4/8-byte field of map m. 8-byte adds go to this

@@ -2402,6 +2402,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   // on no chain, the chains. Returns 1 when the batch has to take the one-lane replay instead (maps,
   // packets and records rolled back), 0 when done (used: XE_MODE_PARALLEL when no packet wrote a map
   // entry, so the SPEC pass was an ordinary parallel run; else XE_MODE_KEYED), < 0 on error.
+  // (tuning build: XE_KEYED_TRACE=1 names why a keyed attempt gave up or started over)
+  auto keyed_trace = [&](const char* why) {
+    if (xe_tuning_env("XE_KEYED_TRACE")) fprintf(stderr, "keyed: %s (n=%u)\n", why, n);
+  };
   auto keyed = [&](uint32_t& used_out) -> int {
     void* kjit = keyed_kernel(vm, jit);  // the per-program kernel's keyed variant
     if (jit && !kjit) return 1;
@@ -2446,12 +2450,13 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (g == 1) {
         if (rollback(false) || prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
         P.maps = vm->d_maps;
+        keyed_trace("spec capacity: grown");
         return 2;
       }
     }
-    if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) return krollback() ? -1 : 1;
+    if (flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY)) { keyed_trace("spec ordered/capacity"); return krollback() ? -1 : 1; }
     if (!(flags & XE_FLAG_KEYED)) {  // no packet wrote a map entry: an ordinary parallel run
-      if (run_conflict(red, P.nmaps)) return krollback() ? -1 : 1;
+      if (run_conflict(red, P.nmaps)) { keyed_trace("spec conflict"); return krollback() ? -1 : 1; }
       if (ordmaps && ordered_finalize(vm, kh0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
       used_out = XE_MODE_PARALLEL;
       return 0;
@@ -2462,7 +2467,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     auto read_small = [&]() { return d2h(small.data(), vm->d_ksmall, XE_KS_WORDS * 4, s) || dsync(s); };
     if (step(XE_KS_DSET, n)) return fail(vm, XE_ERR_DEVICE, "keyed build");
     for (int round = 0;; round++) {
-      if (round >= 64) return krollback() ? -1 : 1;
+      if (round >= 64) { keyed_trace("union rounds"); return krollback() ? -1 : 1; }
       if (dmemset(K.changed, 0, 4, s) || step(XE_KS_UNION, n) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
       if (!small[XE_KS_CHANGED]) break;
     }
@@ -2470,9 +2475,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       return fail(vm, XE_ERR_DEVICE, "keyed build");
     if (small[XE_KS_ERR] & 8u) {  // D outgrew its table: once more with room for every packet's key
       vm->keyed_dnext = dmax;
-      if (dcap < dmax) return krollback() ? -1 : 2;
+      if (dcap < dmax) { keyed_trace("D full"); return krollback() ? -1 : 2; }
     }
-    if (small[XE_KS_ERR]) return krollback() ? -1 : 1;  // key log overflow
+    if (small[XE_KS_ERR]) { keyed_trace("key log overflow"); return krollback() ? -1 : 1; }  // key log overflow
     {
       uint64_t nd = 0;
       for (uint32_t i = 0; i < 64; i++) nd += small[XE_KS_DCOUNT + i];
@@ -2499,10 +2504,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
           m.host_dirty = true;  // the mirror is the batch's start: rebuilt with the larger pool
           if (prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "ordered map room");
           P.maps = vm->d_maps;
+          keyed_trace("LRU pool grown");
           return 2;
         }
       }
-      if (cnt + nd > m.def.max_entries) return krollback() ? -1 : 1;
+      if (cnt + nd > m.def.max_entries) { keyed_trace("capacity"); return krollback() ? -1 : 1; }
     }
     uint32_t end_bit = 1;
     while ((1ull << end_bit) <= K.dcap) end_bit++;
@@ -2515,12 +2521,12 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     // one chain with more than half the packets (a hot key written by most of them): its lane would
     // take longer than the staged one-lane replay of the whole batch
     if (step(XE_KS_CSTART, K.nO) || step(XE_KS_CLONG, K.nO) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed build");
-    if (small[XE_KS_LONG]) return krollback() ? -1 : 1;
+    if (small[XE_KS_LONG]) { keyed_trace("long chain"); return krollback() ? -1 : 1; }
     // 3. back to the start state; reserve a slot record for every new HASH key of D
     if (krollback() || snap_records()) return fail(vm, XE_ERR_DEVICE, "rollback");
     if (ordmaps && step(XE_KS_LRUID, K.dcap)) return fail(vm, XE_ERR_DEVICE, "keyed value ids");
     if (step(XE_KS_RESERVE, K.dcap) || read_small()) return fail(vm, XE_ERR_DEVICE, "keyed reserve");
-    if (small[XE_KS_ERR]) return rollback(true) ? -1 : 1;
+    if (small[XE_KS_ERR]) { keyed_trace("reserve"); return rollback(true) ? -1 : 1; }
     // 4. the packets on no chain, in parallel (the fast kernel: the skip mask is its only keyed input)
     X.mode = XE_MODE_PARALLEL;
     X.K = K;
@@ -2545,7 +2551,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (general && ensure_arena(vm, false, cgrid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     if (klaunch(&X, cgrid) || step(XE_KS_UNNEW, K.dcap)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
     if (read_aux() || read_small()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
-    if (run_conflict(red, P.nmaps)) return rollback(true) ? -1 : 1;  // a packet left its chain / an order-dependent add
+    if (run_conflict(red, P.nmaps)) { keyed_trace("chain conflict"); return rollback(true) ? -1 : 1; }  // a packet left its chain / an order-dependent add
     // the chains' inserts into the map counts (LRU_HASH: header word 2)
     for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];

@@ -2710,12 +2710,24 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     }
     if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
       // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the
-      // keyed path, everything else (and what the keyed path refuses) the replay in packet order
+      // keyed path, everything else (and what the keyed path refuses) the replay in packet order.
+      // A pass that also ran out of an ordered map's room (appends beside an ordered write) grows it
+      // first, so the keyed path does not inherit the shortage.
+      bool grown = false;
+      if (ordmaps && (flags & XE_FLAG_CAPACITY) && (flags & XE_FLAG_ORDERED)) {
+        const int g = ordered_grow(vm, ord_h0, s);  // (restores the ordered maps itself)
+        if (g < 0) return fail(vm, XE_ERR_DEVICE, "ordered map room");
+        grown = g == 1;
+      }
       if (rollback(false)) return fail(vm, XE_ERR_DEVICE, "rollback");
-      if (ordmaps)  // the appends of the run are past the restored counts: unreferenced
+      if (grown) {
+        if (prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+        P.maps = vm->d_maps;
+      } else if (ordmaps) {  // the appends of the run are past the restored counts: unreferenced
         if (ordered_hdr_restore(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "rollback (ordered maps)");
+      }
       int r = 1;
-      const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && !(flags & XE_FLAG_CAPACITY) && !list_conflict;
+      const bool try_keyed = keyed_ok && (flags & XE_FLAG_ORDERED) && (!(flags & XE_FLAG_CAPACITY) || grown) && !list_conflict;
       if (try_keyed && vm->keyed_backoff) vm->keyed_backoff--;
       else if (try_keyed) {
         vm->t2.rec(s);

@@ -10,8 +10,10 @@ line() {  # name args...
   timeout -k 10 240 python bench.py "$@" > $OUT/bench_$n.json 2> $OUT/bench_$n.err || { echo "bench $n failed"; tail -5 $OUT/bench_$n.err; return 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d.get('roofline',{}); print(sys.argv[2], d['value'], d['unit'], r.get('avg_kernel_ms'), r.get('frac'), d.get('verified'))" $OUT/bench_$n.json $n
 }
-line c3 --config c3 $B --no-ordered && line c4 --config c4 $B --no-ordered && line c4f --config c4f $B --no-ordered &&
-line c5 --config c5 $B --no-ordered && line bpf2bpf --config bpf2bpf $B --no-ordered && line c1 --config c1 $B --no-ordered || exit 1
+[ -n "$LINES" ] && { line c3 --config c3 $B --no-ordered && line c4 --config c4 $B --no-ordered && line c4f --config c4f $B --no-ordered &&
+line c5 --config c5 $B --no-ordered && line bpf2bpf --config bpf2bpf $B --no-ordered && line c1 --config c1 $B --no-ordered || exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_ordered_par.py -m gpu -v --maxfail=5 --timeout 200 --timeout-method thread > $OUT/pytest_ordered.log 2>&1; rc=$?
+tail -2 $OUT/pytest_ordered.log; [ $rc -eq 0 ] || { grep -E "FAILED|^E " $OUT/pytest_ordered.log | head; exit 1; }
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 $B --no-ordered --no-c5 > $OUT/prof_c2.log 2>&1 || { echo "prof c2 failed"; tail -3 $OUT/prof_c2.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_bpf2bpf -o run --output-format csv -- python3 bench.py --config bpf2bpf --steps 10 --warmup 2 $B --no-ordered > $OUT/prof_bpf2bpf.log 2>&1 || { echo "prof bpf2bpf failed"; tail -3 $OUT/prof_bpf2bpf.log; exit 1; }
 echo "kernel stats done"

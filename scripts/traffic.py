@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch of the emulator kernel for C2-C5 from the round-3 PMC passes
-(scripts/gpu_r3_pmc.sh: separate rocprofv3 --pmc runs of FETCH_SIZE, WRITE_SIZE and
+"""HBM traffic per launch of the emulator kernel from PMC passes (scripts/gpu_r3_pmc.sh,
+scripts/gpu_r4_configs.sh: separate rocprofv3 --pmc runs of FETCH_SIZE, WRITE_SIZE and
 TCC_EA0_RDREQ_sum + TCC_EA0_ATOMIC_sum over `bench.py --config <c> --steps 5`).
 
-  python scripts/traffic_r3.py <pmc dir (gpurun_out/r3pmc)> <out dir (profiles/r3)>
+  python scripts/traffic.py <pmc dir (gpurun_out/r4cfg)> <out dir (profiles/r4)> [configs: c2 c3 c4 c4f c5]
 
 Correction as MI355X_MICROARCH.md prescribes (HBM/rocprofv3 section): on gfx950 FETCH_SIZE reports half
 of the bytes of wide coalesced streaming reads, so `hbm_bytes_per_launch` = 2 x FETCH_SIZE + WRITE_SIZE.
@@ -18,7 +18,7 @@ import json
 import sys
 from pathlib import Path
 
-PKTS = {"c2": 16777216, "c3": 16777216, "c4": 16777216, "c5": 33554432}
+PKTS = {"c2": 16777216, "c3": 16777216, "c4": 16777216, "c4f": 16777216, "c5": 33554432}
 
 
 def per_launch(d: Path) -> dict:
@@ -37,7 +37,9 @@ def per_launch(d: Path) -> dict:
 def main() -> None:
     src, dst = Path(sys.argv[1]), Path(sys.argv[2])
     dst.mkdir(parents=True, exist_ok=True)
-    for name, n in PKTS.items():
+    names = sys.argv[3:] or list(PKTS)
+    for name in names:
+        n = PKTS[name]
         fetch = per_launch(src / f"{name}_fetch")["FETCH_SIZE"] * 1024
         write = per_launch(src / f"{name}_write")["WRITE_SIZE"] * 1024
         rq = per_launch(src / f"{name}_rdreq")
@@ -57,7 +59,7 @@ def main() -> None:
             "traffic_over_alg": round(hbm / alg, 3),
             "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE reports half of wide streaming reads)",
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ_sum,TCC_EA0_ATOMIC_sum, separate passes of "
-                      f"python3 bench.py --config {name} --packets {n} --steps 5 --warmup 1 (scripts/gpu_r3_pmc.sh)",
+                      f"python3 bench.py --config {name} --packets {n} --steps 5 --warmup 1 ({src})",
         }
         # the round-2 shape calibration (profiles/r2/fetch_size_calibration*.json): streaming parts x2,
         # random probe groups x1, 1500-B-stride windows counted at 0.82 of the 64-B blocks they touch
@@ -65,6 +67,8 @@ def main() -> None:
             cal = fetch + 40 * n  # descriptors + back-to-back windows stream (counted half); probes x1
         elif name == "c4":
             cal = 16 * n + (fetch - 8 * n) / (385.0e6 / 469.8e6)
+        elif name == "c4f":  # frame-aligned windows: one 64-B block per 2-KiB frame (x1, one request each)
+            cal = fetch + 8 * n  # + the descriptors' streaming half
         else:
             cal = fetch + 8 * n  # IMIX: descriptors stream; windows and probes at x1 (a lower bound)
         d["calibrated_estimate"] = {"hbm_bytes_per_packet": round((cal + write) / n, 1),

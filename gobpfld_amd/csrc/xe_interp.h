@@ -1755,6 +1755,14 @@ XE_DEV void lru_unlink(const XeDevMap& M, uint32_t v) {
   if (p != XE_NONE) *lru_link(M, p, 1) = n; else *map_hdr(M, 0) = n;
   if (n != XE_NONE) *lru_link(M, n, 0) = p; else *map_hdr(M, 1) = p;
 }
+// A value's stamp (M.tag[v]): its place in the UsageList as a number, larger = more recently used, 0 =
+// not in the list. Every touch writes the run's epoch (header word 5, set by the host per run) | the
+// packet | the packet's touch count, so the list is also "the live values by stamp, descending": the
+// parallel and keyed runs keep only stamps (lru_touch), and the host rebuilds the links from them on the
+// device when a one-lane replay or a host read needs them (xe_runtime.cpp lru_relink).
+XE_DEV uint64_t lru_stamp(XeLane& L, const XeDevMap& M) {
+  return *map_hdr(M, 5) | (uint64_t(L.pidx) << 16) | (L.oseq++ & 0xffffu);
+}
 XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
   const uint32_t h = uint32_t(*map_hdr(M, 0));
   *lru_link(M, v, 0) = XE_NONE;
@@ -1762,7 +1770,8 @@ XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
   if (h != XE_NONE) *lru_link(M, h, 0) = v; else *map_hdr(M, 1) = v;
   *map_hdr(M, 0) = v;
 }
-XE_DEV void lru_promote(const XeDevMap& M, uint32_t v) {  // promote, :51-68
+XE_DEV void lru_promote(XeLane& L, const XeDevMap& M, uint32_t v) {  // promote, :51-68
+  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp(L, M);
   if (uint32_t(*map_hdr(M, 0)) == v) return;
   lru_unlink(M, v);
   lru_push_front(M, v);
@@ -1772,7 +1781,7 @@ XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_
 // is what the UsageList keeps (the runtime relinks by it, lru_finalize)
 XE_DEV int lru_touch(XeLane& L, const XeDevMap& M, uint32_t v) {
   if (L.oseq >= 0xffffu) return XE_EV_ORD;
-  xe_atomic_max64((unsigned long long*)M.tag + v, ((uint64_t(L.pidx) << 16) | L.oseq++) + 1);
+  xe_atomic_max64((unsigned long long*)M.tag + v, lru_stamp(L, M));
   return 0;
 }
 // LRU lookup of a key (no promotion); value id or XE_NONE
@@ -1782,12 +1791,13 @@ XE_DEV uint32_t lru_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
 }
 // delete, :163-183 (evicted values keep their pool entry: pointers to them stay valid)
 XE_DEV void lru_erase(const XeDevMap& M, uint32_t v) {
+  ((XE_GP(uint64_t))M.tag)[v] = 0;  // out of the list
   const uint32_t slot = *lru_link(M, v, 2);
   ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_TOMB;
   lru_unlink(M, v);
   *map_hdr(M, 2) -= 1;
 }
-XE_DEV int lru_insert(const XeDevMap& M, const uint64_t* kw, bool empty, uint32_t& v) {
+XE_DEV int lru_insert(XeLane& L, const XeDevMap& M, const uint64_t* kw, bool empty, uint32_t& v) {
   const uint64_t nv = *map_hdr(M, 3);
   if (nv >= M.pool_cap) return XE_EV_CAP;
   v = uint32_t(nv);
@@ -1797,6 +1807,7 @@ XE_DEV int lru_insert(const XeDevMap& M, const uint64_t* kw, bool empty, uint32_
   *lru_link(M, v, 2) = uint32_t(slot);
   ((XE_GP(uint32_t))M.elen)[v] = M.value_size;
   *map_hdr(M, 2) += 1;
+  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp(L, M);
   lru_push_front(M, v);  // appended to the UsageList, then promoted to its top (:144-150)
   return 0;
 }
@@ -1914,7 +1925,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
 #endif
         return 0;
       }
-      lru_promote(M, v);
+      lru_promote(L, M, v);
       out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
       return 0;
     }
@@ -2130,12 +2141,12 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     }
 #endif
     if (v == XE_NONE) {
-      if (int e = lru_insert(M, kw, empty, v)) return e;
+      if (int e = lru_insert(L, M, kw, empty, v)) return e;
     } else if (xe_concurrent(P)) {
       if (int e = lru_touch(L, M, v)) return e;  // appended + promoted, or promoted (:144-150)
       if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
     } else {
-      lru_promote(M, v);
+      lru_promote(L, M, v);
       if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
     }
     uint8_t* dst = M.vals + uint64_t(v) * M.value_size;
@@ -3038,6 +3049,10 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
                    xe_readlane(int(f), int(k)) != 0, L.hdrbuf, int(k));
       else
         lane_reset(L, P, c0 + k, valid);
+#if XE_HAS_ORDERED
+      L.pidx = c0 + k;  // order keys of the packet's LRU stamps (lru_stamp)
+      L.oseq = 0;
+#endif
       body(c0 + k, valid);
     }
   }
@@ -3558,6 +3573,7 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   uint64_t steps = 0;
 #if XE_GEN
   L.pidx = i;
+  L.oseq = 0;
 #endif
 #if XE_TRACE
   const int32_t tslot = valid && P.trace ? trace_slot(P, i) : -1;

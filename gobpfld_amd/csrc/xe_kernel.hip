@@ -301,6 +301,52 @@ extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch,
   return hipcub::DeviceScan::ExclusiveSum(scratch, tmp, K->iota, K->ckey, int(n), s) == hipSuccess ? 0 : -1;
 }
 
+// An LRU map's UsageList from its stamps (xe_runtime.cpp lru_relink): the pool's value ids sorted by
+// stamp, descending, then the first cnt of them linked in that order.
+__global__ void xe_iota_kernel(uint32_t* v, uint32_t n) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) v[i] = uint32_t(i);
+}
+__global__ void xe_lru_link_kernel(const uint32_t* order, uint32_t cnt, uint32_t* link, uint64_t* hdr) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cnt; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t v = order[i];
+    link[4 * uint64_t(v)] = i ? order[i - 1] : XE_NONE;
+    link[4 * uint64_t(v) + 1] = i + 1 < cnt ? order[i + 1] : XE_NONE;
+    if (i == 0) hdr[0] = v;
+    if (i + 1 == cnt) hdr[1] = v;
+  }
+}
+__global__ void xe_lru_empty_kernel(uint64_t* hdr) { hdr[0] = XE_NONE; hdr[1] = XE_NONE; }
+extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
+                                    size_t* bytes, hipStream_t s) {
+  // scratch: sorted stamps (pool u64), value ids in / out (pool u32 each), then the sort's own storage
+  const size_t fixed = (size_t(pool) * 16 + 255) & ~size_t(255);
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, int(pool), 0, 64, s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *bytes = fixed + tmp;
+    return 0;
+  }
+  if (*bytes < fixed + tmp || cnt > pool) return -1;
+  if (!cnt || !pool) {
+    hipLaunchKernelGGL(xe_lru_empty_kernel, dim3(1), dim3(1), 0, s, hdr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  uint8_t* b = (uint8_t*)scratch;
+  unsigned long long* keys_out = (unsigned long long*)b;
+  uint32_t* vin = (uint32_t*)(b + size_t(pool) * 8);
+  uint32_t* vout = vin + pool;
+  const uint32_t blocks = pool / 256 + 1 < 8192 ? pool / 256 + 1 : 8192;
+  hipLaunchKernelGGL(xe_iota_kernel, dim3(blocks), dim3(256), 0, s, vin, pool);
+  if (hipGetLastError() != hipSuccess) return -1;
+  if (hipcub::DeviceRadixSort::SortPairsDescending(b + fixed, tmp, (const unsigned long long*)tag, keys_out, vin, vout, int(pool),
+                                                   0, 64, s) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(xe_lru_link_kernel, dim3(blocks), dim3(256), 0, s, vout, cnt, link, hdr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // host-side launchers (called from xe_runtime.cpp)
 extern "C" int xe_launch_interp(const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s) {
   hipLaunchKernelGGL(xe_interp_kernel, dim3(blocks), dim3(threads), (P->nmaps + 1) * sizeof(XeDevMap), s, *P);

@@ -46,6 +46,8 @@ extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* 
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
+                                    size_t* bytes, hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -224,6 +226,20 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, siz
   for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
   return 0;
 }
+int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
+                      size_t* bytes, xe_stream_t) {  // xe_kernel.hip xe_launch_lru_relink
+  if (!scratch) { *bytes = 8; return 0; }
+  std::vector<uint32_t> v(pool);
+  for (uint32_t i = 0; i < pool; i++) v[i] = i;
+  std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return tag[a] > tag[b]; });
+  for (uint32_t i = 0; i < cnt && i < pool; i++) {
+    link[4 * uint64_t(v[i])] = i ? v[i - 1] : XE_NONE;
+    link[4 * uint64_t(v[i]) + 1] = i + 1 < cnt ? v[i + 1] : XE_NONE;
+  }
+  hdr[0] = cnt ? v[0] : XE_NONE;
+  hdr[1] = cnt ? v[cnt - 1] : XE_NONE;
+  return 0;
+}
 int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t) {
   if (!scratch) { *bytes = 8; return 0; }
   uint32_t acc = 0;
@@ -300,6 +316,10 @@ int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes
   return xe_launch_keyed_scan(K, n, scratch, bytes, s);
 }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
+int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
+                      size_t* bytes, xe_stream_t s) {
+  return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, s);
+}
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
 int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
                         xe_stream_t s) {
@@ -641,7 +661,10 @@ struct HostMap {
   uint64_t data_cap = 0;
   uint64_t n_vals = 0, n_elen = 0, n_link = 0, n_rec = 0;  // allocated elements of the device arrays
   uint64_t* d_tag = nullptr;  // QUEUE / STACK / PERF: order keys of a parallel run's appends (pool_cap)
-  uint64_t n_tag = 0;         // LRU: each value's last touch in a parallel run
+  uint64_t n_tag = 0;         // LRU: each value's stamp (xe_interp.h lru_stamp: the UsageList as numbers)
+  uint64_t* d_tsnap = nullptr;  // LRU: the stamps at a parallel run's start (its touches are rolled back)
+  uint64_t n_tsnap = 0;
+  bool links_stale = false;     // LRU: a parallel / keyed run left only stamps (lru_relink rebuilds the links)
   uint8_t* d_vsnap = nullptr; // LRU: the value pool at a parallel run's start (its adds are rolled back)
   uint64_t n_vsnap = 0;
   bool ordered() const { return dkind == XE_DM_LRU || dkind == XE_DM_LIST || dkind == XE_DM_PERF; }
@@ -859,6 +882,8 @@ struct xe_vm {
   uint32_t ord_backoff = 0;
   void* d_app = nullptr; size_t d_app_cap = 0;
   void* d_app_sort = nullptr; size_t d_app_sort_cap = 0;
+  void* d_relink = nullptr; size_t d_relink_cap = 0;  // lru_relink: sort keys / values + scratch
+  uint64_t lru_epoch = 0;  // runs so far: LRU stamps carry it in their top bits (header word 5)
   uint32_t sched = 0;  // chunk -> wave schedule permutation of the parallel passes (xe_debug_set_schedule)
 };
 // ---- keyed ordered execution buffers (XeKeyed), sized for n packets
@@ -1004,6 +1029,10 @@ void map_free_device(HostMap& m) {
   dev_free(m.d_vsnap);
   m.d_vsnap = nullptr;
   m.n_vsnap = 0;
+  dev_free(m.d_tsnap);
+  m.d_tsnap = nullptr;
+  m.n_tsnap = 0;
+  m.links_stale = false;
 }
 
 // Ordered maps on the device (xe_interp.h, general model; XeDevMap comment): rebuilt from the host
@@ -1034,9 +1063,23 @@ int map_upload(xe_vm* vm, HostMap& m) {
   return 0;
 }
 
+int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s) {
+  if (!m.links_stale || m.dkind != XE_DM_LRU) return 0;
+  uint64_t hdr[8];
+  if (d2h(hdr, m.d_hdr, 64, s) || dsync(s)) return -1;
+  size_t bytes = 0;
+  if (launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, nullptr, &bytes, s) ||
+      ensure_buf(&vm->d_relink, &vm->d_relink_cap, bytes) ||
+      launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, vm->d_relink, &bytes, s) || dsync(s))
+    return -1;
+  m.links_stale = false;
+  return 0;
+}
+
 int map_download(xe_vm* vm, HostMap& m) {
   if (!m.dev_dirty) return 0;
   if (m.ordered()) {
+    if (m.dkind == XE_DM_LRU && lru_relink(vm, m, vm->stream)) return -1;
     if (ordered_download(vm, m)) return -1;
     m.dev_dirty = false;
     return 0;
@@ -1124,6 +1167,7 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
       if (!m.d_keys && dev_alloc((void**)&m.d_keys, rec.size() * 8)) return -1;
       if (h2d(m.d_keys, rec.data(), rec.size() * 8, st)) return -1;
       hdr[0] = n ? 0 : XE_NONE; hdr[1] = n ? n - 1 : XE_NONE; hdr[2] = n; hdr[3] = n;
+      hdr[5] = vm->lru_epoch << 40;  // the stamp base of the run in progress (xe_interp.h lru_stamp)
     } else {  // QUEUE / STACK: element i is Values[i]; the list starts at 0
       link.resize(pool);
       for (uint64_t i = 0; i < pool; i++) link[i] = uint32_t(i);
@@ -1139,7 +1183,12 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
       return -1;
   }
   if (ensure_dev(&m.d_tag, m.n_tag, m.pool_cap)) return -1;
-  if (m.dkind == XE_DM_LRU && dmemset(m.d_tag, 0, uint64_t(m.pool_cap) * 8, st)) return -1;  // no touches yet
+  if (m.dkind == XE_DM_LRU) {  // stamps in UsageList order (epoch 0: every run's touches are newer)
+    std::vector<uint64_t> tag(m.pool_cap, 0);
+    for (uint64_t i = 0; i < n; i++) tag[i] = n - i;
+    if (h2d(m.d_tag, tag.data(), tag.size() * 8, st) || dsync(st)) return -1;
+    m.links_stale = false;
+  }
   if (!m.d_hdr && dev_alloc((void**)&m.d_hdr, 8 * 8)) return -1;
   if (h2d(m.d_hdr, hdr.data(), 64, st) || dsync(st)) return -1;
   m.host_dirty = false;
@@ -1423,7 +1472,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
   dev_free(vm->d_arena_par); dev_free(vm->d_arena_seq); dev_free(vm->d_ksnap);
   dev_free(vm->d_umem); dev_free(vm->d_desc); dev_free(vm->d_res); dev_free(vm->d_ver); dev_free(vm->d_regs);
-  dev_free(vm->d_usnap); dev_free(vm->d_ovl); dev_free(vm->d_app); dev_free(vm->d_app_sort);
+  dev_free(vm->d_usnap); dev_free(vm->d_ovl); dev_free(vm->d_app); dev_free(vm->d_app_sort); dev_free(vm->d_relink);
   keyed_free(vm);
   vm->t0.fini(); vm->t1.fini(); vm->t2.fini();
 #ifndef XE_HOSTSIM
@@ -1886,6 +1935,9 @@ static int ordered_hdr_read(xe_vm* vm, std::vector<uint64_t>& out, xe_stream_t s
     if (snap_pools && m.dkind == XE_DM_LRU) {
       const uint64_t vb = uint64_t(m.pool_cap) * m.def.value_size;
       if (ensure_dev(&m.d_vsnap, m.n_vsnap, vb) || (vb && d2d(m.d_vsnap, m.d_vals, vb, s))) return -1;
+      if (ensure_dev(&m.d_tsnap, m.n_tsnap, m.pool_cap) ||
+          (m.pool_cap && d2d(m.d_tsnap, m.d_tag, uint64_t(m.pool_cap) * 8, s)))
+        return -1;
     }
   }
   return dsync(s);
@@ -1895,44 +1947,26 @@ static int ordered_hdr_restore(xe_vm* vm, const std::vector<uint64_t>& h, xe_str
   for (size_t i = 1; i < vm->maps.size(); i++) {
     HostMap& m = vm->maps[i];
     if (m.ordered() && h2d(m.d_hdr, &h[i * 8], 64, s)) return -1;
-    if (m.dkind == XE_DM_LRU && m.d_tag && dmemset(m.d_tag, 0, uint64_t(m.pool_cap) * 8, s)) return -1;
+    if (m.dkind == XE_DM_LRU && m.d_tag && m.d_tsnap && m.pool_cap &&
+        d2d(m.d_tag, m.d_tsnap, uint64_t(m.pool_cap) * 8, s))
+      return -1;
     const uint64_t vb = uint64_t(m.pool_cap) * m.def.value_size;
     if (m.dkind == XE_DM_LRU && vb && d2d(m.d_vals, m.d_vsnap, vb, s)) return -1;
   }
   return dsync(s);
 }
-// The promotions of a parallel run's LRU lookups: in packet order every touched key ends up ahead of
-// the untouched ones, the most recently touched first (maps_hash_lru.go:51-68 per lookup). The run left
-// each value's last touch in its tag; the UsageList (device links) is rebuilt from them and the tags
-// are cleared for the next run.
-static int lru_finalize(xe_vm* vm, HostMap& m, xe_stream_t s) {
-  const uint32_t pool = m.pool_cap;
-  std::vector<uint64_t> tag(pool);
-  if (pool && (d2h(tag.data(), m.d_tag, uint64_t(pool) * 8, s) || dsync(s))) return -1;
-  std::vector<std::pair<uint64_t, uint32_t>> touched;
-  for (uint32_t v = 0; v < pool; v++)
-    if (tag[v]) touched.push_back({tag[v], v});
-  if (touched.empty()) return 0;
-  std::vector<uint64_t> hdr(8);
-  std::vector<uint32_t> link(4 * uint64_t(pool));
-  if (d2h(hdr.data(), m.d_hdr, 64, s) || d2h(link.data(), m.d_link, link.size() * 4, s) || dsync(s)) return -1;
-  std::vector<uint32_t> order;
-  order.reserve(hdr[2]);
-  std::sort(touched.begin(), touched.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-  for (const auto& t : touched) order.push_back(t.second);
-  for (uint32_t v = uint32_t(hdr[0]); v != XE_NONE && order.size() <= hdr[2] + touched.size(); v = link[4 * uint64_t(v) + 1])
-    if (!tag[v]) order.push_back(v);
-  for (size_t i = 0; i < order.size(); i++) {
-    link[4 * uint64_t(order[i])] = i ? order[i - 1] : XE_NONE;
-    link[4 * uint64_t(order[i]) + 1] = i + 1 < order.size() ? order[i + 1] : XE_NONE;
-  }
-  hdr[0] = order.empty() ? XE_NONE : order.front();
-  hdr[1] = order.empty() ? XE_NONE : order.back();
-  if (h2d(m.d_link, link.data(), link.size() * 4, s) || h2d(m.d_hdr, hdr.data(), 64, s) ||
-      dmemset(m.d_tag, 0, uint64_t(pool) * 8, s) || dsync(s))
-    return -1;
+// The promotions of a parallel / keyed run's LRU touches: every touch left its stamp (epoch | packet |
+// touch count) with an atomic max, so the UsageList is now "the live values by stamp, descending" — in
+// packet order every touched key ended up ahead of the untouched ones, the most recently touched first
+// (maps_hash_lru.go:51-91 per touch). Nothing to do until something needs the links (lru_relink).
+static int lru_finalize(xe_vm*, HostMap& m, xe_stream_t) {
+  m.links_stale = true;
   return 0;
 }
+
+// Rebuild an LRU map's UsageList links from the stamps on the device: the pool sorted by stamp,
+// descending (radix sort), its first `count` values linked in that order (head = most recent). Before
+// a one-lane replay (it promotes and evicts through the links) and before the host reads the map.
 
 // put the appends of a parallel run (header words `h0` before it) into packet order
 static int ordered_finalize(xe_vm* vm, const std::vector<uint64_t>& h0, uint32_t n, xe_stream_t s) {
@@ -2265,6 +2299,15 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
 
   XeParams P = batch_params(vm, d_umem, umem_len, d_desc, n, d_results, d_verdicts, d_regs, vm->d_aux);
   const size_t aux_used = 16 + size_t(kRep) * P.rep_words;
+  // LRU stamps of this run sort after every earlier run's (xe_interp.h lru_stamp; header word 5)
+  {
+    bool lru = false;
+    for (size_t i = 1; i < vm->maps.size(); i++) lru = lru || vm->maps[i].dkind == XE_DM_LRU;
+    const uint64_t e = lru ? (++vm->lru_epoch) << 40 : 0;
+    for (size_t i = 1; i < vm->maps.size(); i++)
+      if (vm->maps[i].dkind == XE_DM_LRU && (h2d(vm->maps[i].d_hdr + 5, &e, 8, s) || dsync(s)))
+        return fail(vm, XE_ERR_DEVICE, "LRU epoch");
+  }
   if (P.trace && dmemset(vm->d_trace_cnt, 0, vm->trace_pk.size() * 4, s)) return fail(vm, XE_ERR_DEVICE, "trace reset");
   // host functions are called in packet order only
   const bool hostcalls = calls_host_helper(vm);
@@ -2366,6 +2409,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
       if (m.ordered() && map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
+      if (m.dkind == XE_DM_LRU && lru_relink(vm, m, s)) return fail(vm, XE_ERR_DEVICE, "LRU relink");  // it promotes / evicts
     }
     // the replay lane's packets are staged 64 at a time by the whole wave unless a packet may write
     // packet bytes a later packet reads (its window must then be fetched after the earlier writes)

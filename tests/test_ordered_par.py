@@ -289,3 +289,43 @@ def test_c3lru_device_keyed_equals_oracle(gpu_lib, oracle_lib):
     got = _c3lru_run(gpu_lib, n)
     assert got[0].stats["mode_used"] == MODE_KEYED, got[0].stats
     _same_c3lru(got, _c3lru_run(oracle_lib, n))
+
+
+def _lru_mixed_stream(lib, n=512):
+    """Batches that alternate the LRU paths: lookups only (parallel: stamps), learning inserts (keyed
+    chains), updates that evict (the one-lane replay: it needs the links rebuilt from the stamps). The
+    UsageList and the values after every batch are compared with the oracle's single VM."""
+    from gobpfld_amd.emulator import VM, Settings
+    vm = VM(Settings(), lib=lib)
+    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 8, 56))  # 48 preloaded: a batch that learns past 8 keys evicts
+    for k, v in LRU_PRELOAD[0]:
+        vm.map_update(m, k, v)
+    progs = {"lookup": vm.add_raw_program(prog_lru()), "learn": vm.add_raw_program(prog_lru(update=True))}
+    out = []
+    # (after a replay the next 8 batches replay too: the back-off, xe_runtime.cpp kKeyedBackoff)
+    for b, kind in enumerate(["lookup", "learn"] + ["lookup"] * 10 + ["learn"] + ["lookup"] * 10):
+        umem, descs = packets(n, 64, seed=100 + b)
+        vm.set_entrypoint(progs[kind])
+        r = vm.run_batch(umem, descs, want_regs=True)
+        out.append((r.results.copy(), vm.map_lru_order(m), vm.map_dump(m), r.stats["mode_used"]))
+    vm.close()
+    return out
+
+
+def test_lru_stamps_across_paths_hostsim(oracle_lib, hostsim_lib):
+    got, want = _lru_mixed_stream(hostsim_lib), _lru_mixed_stream(oracle_lib)
+    for b, (g, w) in enumerate(zip(got, want)):
+        assert (g[0] == w[0]).all(), f"batch {b}: results"
+        assert g[1] == w[1], f"batch {b}: UsageList"
+        assert np.array_equal(g[2][0], w[2][0]) and np.array_equal(g[2][1], w[2][1]), f"batch {b}: entries"
+    modes = [g[3] for g in got]
+    assert modes[0] == MODE_PARALLEL and modes[1] == MODE_SEQUENTIAL and modes[11] == MODE_PARALLEL, modes
+
+
+@pytest.mark.gpu
+def test_lru_stamps_across_paths_device(gpu_lib, oracle_lib):
+    got, want = _lru_mixed_stream(gpu_lib, 4096), _lru_mixed_stream(oracle_lib, 4096)
+    for b, (g, w) in enumerate(zip(got, want)):
+        assert (g[0] == w[0]).all(), f"batch {b}: results"
+        assert g[1] == w[1], f"batch {b}: UsageList"
+        assert np.array_equal(g[2][0], w[2][0]) and np.array_equal(g[2][1], w[2][1]), f"batch {b}: entries"

@@ -1722,9 +1722,15 @@ XE_DEV bool hash_reserve(const XeDevMap& M, const uint64_t* kw, uint64_t hi = 0)
 #endif
 
 // read a key through a pointer register into zero-padded words; ReadRange errors give the nil key
-// (maps_hash.go:50-53). Returns a panic code or 0.
+// (maps_hash.go:50-53). Returns a panic code or 0. `kp`: the key words a per-program kernel proved
+// equal to what the ReadRange returns (xe_jit.cpp key_shadows) — taken as they are.
 XE_DEV int read_key(XeLane& L, const XeParams& P, const XeReg& R, const XeDevMap& M, uint64_t* kw, bool& empty,
-                    uint32_t cm = XE_CM_ALL) {
+                    uint32_t cm = XE_CM_ALL, const uint64_t* kp = nullptr) {
+  if (kp) {
+    for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = kp[w];
+    empty = false;
+    return 0;
+  }
   for (int w = 0; w < XE_MAX_KEY / 8; w++) kw[w] = 0;
   int e = ptr_read_range(L, P, R, int64_t(M.key_size), [&](int64_t i, uint8_t b) {
     kw[i >> 3] |= uint64_t(b) << (8 * (i & 7));
@@ -1880,7 +1886,7 @@ XE_DEV int in_helper(int e) { return (e & 0xf000) ? e : (e | XE_E_IN_HELPER); }
 // maps_hash_lru.go:70-91, QueueMap/StackMap.Lookup maps_queue.go:39-58 / maps_stack.go:38-58,
 // PerfEventArray.Lookup maps_perf_event_array.go:45-65. `peek`: the key is bpf_map_peek_elem's IMM 0.
 XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, bool peek, XeReg& out, int64_t& err,
-                      uint32_t cm2 = XE_CM_ALL) {
+                      uint32_t cm2 = XE_CM_ALL, const uint64_t* kp = nullptr) {
   const XeDevMap M = map_desc(L, m);
   err = 0;
   out = XeReg{0, 0, XE_KIND_IMM};
@@ -1902,7 +1908,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
   if ((XE_HAS_HASH && M.kind == XE_DM_HASH) || (XE_HAS_ORDERED && M.kind == XE_DM_LRU)) {
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2)) return e;
+    if (int e = peek ? peek_key(M, kw, empty) : read_key(L, P, K, M, kw, empty, cm2, kp)) return e;
 #if XE_KEYED
     uint64_t kid = 0;
     if ((M.kind == XE_DM_HASH || M.kind == XE_DM_LRU) && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)) {
@@ -1976,13 +1982,14 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
 }
 
 // MapLookupElement, helper_functions.go:46-73
-XE_DEV int helper_lookup(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL) {
+XE_DEV int helper_lookup(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
+                         const uint64_t* kp = nullptr) {
   uint32_t m;
   if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
   if (!m) return 0;
   XeReg out;
   int64_t err;
-  if (int e = map_lookup(L, P, m, reg_get(L, 2), false, out, err, cm2)) return in_helper(e);
+  if (int e = map_lookup(L, P, m, reg_get(L, 2), false, out, err, cm2, kp)) return in_helper(e);
   if (err) return helper_errno_result(L, err);
   reg_put(L, 0, out);
   return 0;
@@ -2000,7 +2007,7 @@ XE_DEV int read_value_into(XeLane& L, const XeParams& P, const XeReg& R, int64_t
 
 // MapUpdateElement, helper_functions.go:76-101
 XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
-                         uint32_t cm3 = XE_CM_ALL) {
+                         uint32_t cm3 = XE_CM_ALL, const uint64_t* kp = nullptr) {
   uint32_t m;
   if (int e = reg_to_map(L, P, m, cm1)) return in_helper(e);
   if (!m) return 0;
@@ -2035,7 +2042,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     if (!XE_ISPTR(R2.t)) return helper_errno_result(L, -14);
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
+    if (int e = read_key(L, P, R2, M, kw, empty, cm2, kp)) return e;
 #if XE_KEYED
     const uint64_t kid = kid_hash(m, M, kw, empty);
     if (int e = key_touch(L, P, kid, false)) return e;  // presence (and the count) are read
@@ -2745,6 +2752,15 @@ XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1
     fn = F.v;
   }
   return call_helper(L, P, fn, cm1, cm2, cm3);
+}
+
+// bpf_map_lookup_elem / bpf_map_update_elem of a HASH map whose key words the per-program kernel
+// built from the registers it stored into the frame (xe_jit.cpp key_shadows proves them equal to the
+// ReadRange of R2); everything else about the call is call_helper's (ids 1 and 2 are never replaced
+// in a per-program kernel: a VM with a host or nil helper runs on the interpreter).
+XE_DEV int uop_helper_key(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1, uint32_t cm2, uint32_t cm3,
+                          const uint64_t* kp) {
+  return u.imm == 1 ? helper_lookup(L, P, cm1, cm2, kp) : helper_update(L, P, cm1, cm2, cm3, kp);
 }
 
 #if XE_GEN

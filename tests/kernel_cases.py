@@ -47,6 +47,8 @@ def gpu_cases():
     import test_ref_examples as R
     for prog in (R.from_text(), R.from_literals()):
         cases.append((prog, [R.STATS_MAP], None, Settings(engine=JIT)))
+    import test_key_shadow as KS
+    cases += KS.kernel_cases()
     return cases
 
 

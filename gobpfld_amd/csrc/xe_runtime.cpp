@@ -855,6 +855,7 @@ struct xe_vm {
   void* d_ksort = nullptr;
   size_t d_ksort_cap = 0;
   bool keyed_hint = false;
+  bool keyed_hint_set = false;  // the first batch's hint was derived from the program (lru_update_sites)
   // after the keyed path refused a batch, the next kKeyedBackoff order-dependent batches go straight to
   // the replay (a program whose batches keep refusing does not pay the SPEC pass every time)
   uint32_t keyed_backoff = 0;
@@ -1139,7 +1140,12 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
     hdr[0] = n; hdr[1] = used;
     if (h2d(m.d_rec, rec.data(), rec.size() * 8, st) || h2d(m.d_vals, data.data(), data.size(), st)) return -1;
   } else {
-    const uint64_t pool = n + slack;
+    // An LRU_HASH's value pool starts with room for MaxEntries values (up to 256 MB of them): a batch that
+    // learns many flows then finds its value ids instead of growing the pool and starting over (a full
+    // download / upload of the map and a second SPEC pass: ~50 ms of a 4M-packet C3-LRU batch).
+    uint64_t room = 0;
+    if (m.dkind == XE_DM_LRU) room = std::min<uint64_t>(m.def.max_entries, (256ull << 20) / std::max<uint32_t>(vs, 1));
+    const uint64_t pool = std::max(n, room) + slack;
     std::vector<uint8_t> vals(std::max<uint64_t>(pool * vs, 8), 0);
     std::vector<uint32_t> elen(pool, 0);
     for (uint64_t i = 0; i < n; i++) {
@@ -2039,6 +2045,18 @@ static int ordered_grow(xe_vm* vm, const std::vector<uint64_t>& h0, xe_stream_t 
   return 1;
 }
 
+// the entry program calls bpf_map_update_elem and the VM has an LRU_HASH: such an update never runs in
+// the plain parallel pass (LRU inserts and updates take the keyed path), and rolling a failed pass back
+// rebuilds the ordered maps from the host mirror, so the VM's first batch starts with the keyed path
+static bool lru_update_sites(const xe_vm* vm) {
+  bool lru = false;
+  for (size_t i = 1; i < vm->maps.size(); i++) lru = lru || vm->maps[i].dkind == XE_DM_LRU;
+  if (!lru || vm->entry < 1 || size_t(vm->entry) >= vm->programs.size()) return false;
+  for (const XeUop& u : vm->programs[size_t(vm->entry)])
+    if (u.cls == U_HELPER && u.imm == 2) return true;
+  return false;
+}
+
 static bool has_ordered_maps(const xe_vm* vm) {
   for (size_t i = 1; i < vm->maps.size(); i++)
     if (vm->maps[i].ordered()) return true;
@@ -2629,6 +2647,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   // ordered maps: appends and LRU lookups run in parallel (put in packet order afterwards), LRU updates
   // through the keyed path; a batch with any other operation on them (pops, peeks, list lookups, an LRU
   // eviction) replays in order, and so do the next few after such a batch
+  if (!vm->keyed_hint_set) {
+    vm->keyed_hint_set = true;
+    if (lru_update_sites(vm)) vm->keyed_hint = true;
+  }
   const bool ord_par = !ordmaps || ordered_parallel_ok(vm);
   const bool keyed_ok = mode == XE_MODE_AUTO && n > 0 && !overlap && ord_par;
   bool ord_seq = mode == XE_MODE_AUTO && ordmaps && (!ord_par || vm->ord_backoff);

@@ -91,10 +91,16 @@ def k_overwrite(a):  # a byte of an 8-byte store overwritten: the rest reads as 
     a.st(1, 10, -13, 0x55)
 
 
-def k_alias(a):  # LDX makes R4 alias the stored object; the in-place add changes the key
+def k_alias(a):  # LDX makes R4 alias the stored object; the in-place add changes the key (all 8 bytes)
     k_wide(a)
     a.ldx(4, 4, 10, -16)
     a.add64(4, 1)
+
+
+def k_alias_replaced(a):  # ADD of a pointer replaces R4 instead (inst_add.go:82-98): the object stays
+    k_wide(a)
+    a.ldx(4, 4, 10, -16)
+    a.add64(4, src=10)
 
 
 def k_unwritten(a):  # the last four key bytes were never written (object 0 reads as zero)
@@ -133,7 +139,8 @@ CASES = {
     "update": (k_wide, 2, 16, True, None),
     "straddle": (k_straddle, 1, 16, False, lambda p: p[0:4] + p[8:12] + p[8:16]),
     "overwrite": (k_overwrite, 1, 16, False, lambda p: p[0:4] + p[0:4] + p[8:16]),
-    "alias": (k_alias, 1, 16, False, None),
+    "alias": (k_alias, 1, 16, True, lambda p: ((int.from_bytes(p[0:8], "little") + 1) % 2**64).to_bytes(8, "little") + p[8:16]),
+    "alias_replaced": (k_alias_replaced, 1, 16, False, lambda p: p[0:16]),
     "unwritten": (k_unwritten, 1, 16, False, lambda p: p[0:12] + b"\0\0\0\0"),
     "two_preds": (k_two_preds, 1, 16, False, lambda p: p[0:16]),
     "helper_between": (k_helper_between, 1, 16, False, lambda p: p[0:16]),
@@ -203,11 +210,11 @@ def test_generator_accepts_exactly_the_proven_keys(hostsim_lib, name):
 
 def test_config_kernels_use_key_shadows(hostsim_lib):
     """C3 and C5 look their 5-tuple up through a key shadow and store nothing into the frame; C3-learn's
-    update does not (its key's saddr object is changed in place through an aliasing register before the
-    call, emulator/memory.go:37-52)."""
+    update too, with its key's saddr object changed in place through an aliasing register before the call
+    (emulator/memory.go:37-52): the shadow takes the register's new value."""
     from gobpfld_amd import aot
     from gobpfld_amd import workloads as W
-    for name, sites in (("c3", 1), ("c5", 1), ("c3learn", 1), ("c2", 0), ("bpf2bpf", 0)):
+    for name, sites in (("c3", 1), ("c5", 1), ("c3learn", 2), ("c2", 0), ("bpf2bpf", 0)):
         srcs = aot.sources([lambda vm, n=name: W.setup_vm(vm, n)], lib=hostsim_lib, variants=(0,))
         body = srcs[0].split("XE_DEV void xe_jit_body")[1]
         assert body.count("uop_helper_key(L") == sites, name

@@ -100,7 +100,7 @@ def k_alias(a):  # LDX makes R4 alias the stored object; the in-place add change
 def k_alias_replaced(a):  # ADD of a pointer replaces R4 instead (inst_add.go:82-98): the object stays
     k_wide(a)
     a.ldx(4, 4, 10, -16)
-    a.add64(4, src=10)
+    a.add64(4, src=6)
 
 
 def k_unwritten(a):  # the last four key bytes were never written (object 0 reads as zero)

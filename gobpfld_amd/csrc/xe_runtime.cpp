@@ -2307,11 +2307,19 @@ void note_run(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t mo
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
+  // (tuning build: XE_HOST_TIMING=1 prints host-side marks of the batch, milliseconds since its start)
+  const auto tm0 = std::chrono::steady_clock::now();
+  auto tmark = [&](const char* what) {
+    if (xe_tuning_env("XE_HOST_TIMING"))
+      fprintf(stderr, "host %-14s %8.3f ms (n=%u)\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tm0).count(), n);
+  };
   vm->staged_slot = -1;  // this run writes the maps outside the pipeline
   if (stats) memset(stats, 0, sizeof *stats);
   if (int rc = xe_sync(vm)) return rc;  // pipelined batches first: they precede this one
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
   if (int rc = prepare_run(vm, s)) return rc;
+  tmark("prepare_run");
   if (n && (!d_umem || !d_desc)) return fail(vm, XE_ERR_INVAL, "null umem/desc");
   vm->delta_base = true;
 
@@ -2477,7 +2485,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     while (dmax < 2ull * n && dmax < (1u << 30)) dmax <<= 1;
     const uint64_t dwant = vm->keyed_dnext ? vm->keyed_dnext : std::max<uint64_t>(4096, n / 4);
     while (dcap < dwant && dcap < dmax) dcap <<= 1;
+    tmark("keyed start");
     if (keyed_alloc(vm, n, dcap)) return fail(vm, XE_ERR_NOMEM, "device alloc (keyed execution)");
+    tmark("keyed alloc");
     // ordered maps (LRU_HASH keys, appends): the host mirror holds the batch's start (rollback(true)
     // rebuilds the device copies from it), kh0 their header words / LRU value pools for the cheaper
     // rollbacks before any record was claimed
@@ -2485,7 +2495,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (ordmaps) {
       for (size_t i = 1; i < vm->maps.size(); i++)
         if (vm->maps[i].ordered() && map_download(vm, vm->maps[i])) return fail(vm, XE_ERR_DEVICE, "map download");
+      tmark("map download");
       if (ordered_hdr_read(vm, kh0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
+      tmark("hdr read");
     }
     auto krollback = [&]() -> int {
       if (rollback(false)) return -1;
@@ -2498,6 +2510,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     const uint32_t grid = parallel_grid(vm, kjit, general, n, P.nmaps);
     XeParams X = P;
     if (general && ensure_arena(vm, false, grid * 256, X.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
+    tmark("arena");
     // 1. SPEC: every packet against the start state, writes held back, keys logged
     X.mode = XE_MODE_SPEC;
     X.K = K;
@@ -2647,7 +2660,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   // ordered maps: appends and LRU lookups run in parallel (put in packet order afterwards), LRU updates
   // through the keyed path; a batch with any other operation on them (pops, peeks, list lookups, an LRU
   // eviction) replays in order, and so do the next few after such a batch
-  if (!vm->keyed_hint_set) {
+  tmark("setup");
+  if (!vm->keyed_hint_set && n > 0) {
     vm->keyed_hint_set = true;
     if (lru_update_sites(vm)) vm->keyed_hint = true;
   }
@@ -2839,7 +2853,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       }
     }
   }
-  vm->keyed_hint = used == XE_MODE_KEYED;
+  if (n > 0) vm->keyed_hint = used == XE_MODE_KEYED;  // (an empty batch, e.g. a map upload, says nothing)
   if (used == XE_MODE_KEYED) red[0] |= XE_FLAG_ORDERED;  // order-dependent effects (shard checks replay it)
   record_widths(vm, red, P.nmaps);
   if (used == XE_MODE_SEQUENTIAL || used == XE_MODE_KEYED) {

@@ -2866,7 +2866,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (vm->maps[i].dkind == XE_DM_HASH) vm->maps[i].live = counts[i];
   }
   note_run(vm, red, used);
-  for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
+  if (n > 0)  // an empty batch (a map upload) changes no map: the host mirrors stay current
+    for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   if (stats) {
     stats->packets = n;
     stats->steps = red[1];

@@ -11,6 +11,21 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 PRODUCT_LIB = ROOT / "gobpfld_amd" / "libxdpemu.so"
+TUNING_LIB = ROOT / "gobpfld_amd" / "libxdpemu_tuning.so"  # -DXE_TUNING debug build (scripts/ A/B runs)
+
+
+def product_path() -> Path:
+    """The product library, or — only when XE_LIB names it — the tuning build of the same sources
+    (`python -m gobpfld_amd.build --tuning`). Nothing else may stand in for the product: XE_LIB naming
+    any other file (the host simulation, the oracle, a stray copy) is an error, not a silent swap."""
+    import os
+    env = os.environ.get("XE_LIB")
+    if not env:
+        return PRODUCT_LIB
+    p = Path(env).resolve()
+    if p not in (PRODUCT_LIB.resolve(), TUNING_LIB.resolve()):
+        raise RuntimeError(f"XE_LIB={env}: only {PRODUCT_LIB.name} or {TUNING_LIB.name} may serve as the product library")
+    return p
 
 
 class Desc(C.Structure):  # xsk.go:695-701
@@ -109,6 +124,7 @@ _SIGS = {
     "reset_helper": (C.c_int, [P, C.c_uint32]),
     "prepare": (C.c_int, [P]),
     "debug_set_schedule": (C.c_int, [P, C.c_uint32]),
+    "debug_set_lru_epoch": (C.c_int, [P, C.c_uint64]),
     "set_kernel_cache": (C.c_int, [C.c_char_p]),
     "kernel_source": (C.c_int, [P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "compile_kernel_source": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
@@ -149,6 +165,7 @@ HEADER_SYMBOLS = [
     "xe_device_count", "xe_shard_check", "xe_epoch_begin", "xe_epoch_end", "xe_map_state_bytes", "xe_map_state_export",
     "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error", "xe_debug_set_schedule",
+    "xe_debug_set_lru_epoch",
     "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source", "xe_kernel_object_name",
     "xe_cancel", "xe_trace_config", "xe_trace_read", "xe_set_helper", "xe_reset_helper",
 ]
@@ -184,12 +201,11 @@ def product() -> Lib:
     """The HIP product library. Raises if it is not built — there is no CPU fallback."""
     global _product
     if _product is None:
-        import os
         try:  # torch bundles its own HIP runtime: have it loaded first so the process holds one
             import torch  # noqa: F401
         except ImportError:
             pass
-        _product = Lib(os.environ.get("XE_LIB", PRODUCT_LIB), "xe_")
+        _product = Lib(product_path(), "xe_")
         # the package's ahead-of-time kernel cache (gobpfld_amd/aot.py), when it was built
         kdir = ROOT / "gobpfld_amd" / "kernels"
         if kdir.is_dir() and _product.has("set_kernel_cache"):

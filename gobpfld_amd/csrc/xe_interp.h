@@ -1762,12 +1762,21 @@ XE_DEV void lru_unlink(const XeDevMap& M, uint32_t v) {
   if (n != XE_NONE) *lru_link(M, n, 0) = p; else *map_hdr(M, 1) = p;
 }
 // A value's stamp (M.tag[v]): its place in the UsageList as a number, larger = more recently used, 0 =
-// not in the list. Every touch writes the run's epoch (header word 5, set by the host per run) | the
-// packet | the packet's touch count, so the list is also "the live values by stamp, descending": the
-// parallel and keyed runs keep only stamps (lru_touch), and the host rebuilds the links from them on the
-// device when a one-lane replay or a host read needs them (xe_runtime.cpp lru_relink).
+// not in the list. Every touch writes the run's epoch (header word 5 = epoch << 48, set by the host per
+// run) plus a number that grows in packet order within the run, so the list is also "the live values by
+// stamp, descending": the parallel and keyed runs keep only stamps (lru_touch), and the host rebuilds the
+// links from them on the device when a one-lane replay or a host read needs them (xe_runtime.cpp
+// lru_relink). The fields never overlap: a concurrent touch adds packet << 16 | touch (packet < 2^32,
+// touch < 2^16, lru_touch sends a packet's 65,536th touch to the replay); the one lane walking the batch
+// in order counts its touches in header word 6 instead (< 2^48, no per-packet limit). The host renumbers
+// every stamp before the 16-bit epoch would wrap (xe_runtime.cpp lru_renumber).
 XE_DEV uint64_t lru_stamp(XeLane& L, const XeDevMap& M) {
   return *map_hdr(M, 5) | (uint64_t(L.pidx) << 16) | (L.oseq++ & 0xffffu);
+}
+XE_DEV uint64_t lru_stamp_seq(const XeDevMap& M) {  // one lane, packet order: the run's touch counter
+  const uint64_t c = *map_hdr(M, 6) + 1;
+  *map_hdr(M, 6) = c;
+  return *map_hdr(M, 5) | (c & ((1ull << 48) - 1));
 }
 XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
   const uint32_t h = uint32_t(*map_hdr(M, 0));
@@ -1777,7 +1786,7 @@ XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
   *map_hdr(M, 0) = v;
 }
 XE_DEV void lru_promote(XeLane& L, const XeDevMap& M, uint32_t v) {  // promote, :51-68
-  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp(L, M);
+  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp_seq(M);
   if (uint32_t(*map_hdr(M, 0)) == v) return;
   lru_unlink(M, v);
   lru_push_front(M, v);
@@ -1813,7 +1822,7 @@ XE_DEV int lru_insert(XeLane& L, const XeDevMap& M, const uint64_t* kw, bool emp
   *lru_link(M, v, 2) = uint32_t(slot);
   ((XE_GP(uint32_t))M.elen)[v] = M.value_size;
   *map_hdr(M, 2) += 1;
-  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp(L, M);
+  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp_seq(M);
   lru_push_front(M, v);  // appended to the UsageList, then promoted to its top (:144-150)
   return 0;
 }

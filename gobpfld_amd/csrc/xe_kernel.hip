@@ -302,13 +302,16 @@ extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch,
 }
 
 // An LRU map's UsageList from its stamps (xe_runtime.cpp lru_relink): the pool's value ids sorted by
-// stamp, descending, then the first cnt of them linked in that order.
+// stamp, descending, then the first cnt of them linked in that order; `renumber` also rewrites the
+// stamps as their ranks from the tail (cnt .. 1: epoch 0, below every later run's stamps).
 __global__ void xe_iota_kernel(uint32_t* v, uint32_t n) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) v[i] = uint32_t(i);
 }
-__global__ void xe_lru_link_kernel(const uint32_t* order, uint32_t cnt, uint32_t* link, uint64_t* hdr) {
+__global__ void xe_lru_link_kernel(const uint32_t* order, uint32_t cnt, uint32_t* link, uint64_t* hdr, uint64_t* tag,
+                                   int renumber) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cnt; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t v = order[i];
+    if (renumber) tag[v] = cnt - i;
     link[4 * uint64_t(v)] = i ? order[i - 1] : XE_NONE;
     link[4 * uint64_t(v) + 1] = i + 1 < cnt ? order[i + 1] : XE_NONE;
     if (i == 0) hdr[0] = v;
@@ -317,7 +320,7 @@ __global__ void xe_lru_link_kernel(const uint32_t* order, uint32_t cnt, uint32_t
 }
 __global__ void xe_lru_empty_kernel(uint64_t* hdr) { hdr[0] = XE_NONE; hdr[1] = XE_NONE; }
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
-                                    size_t* bytes, hipStream_t s) {
+                                    size_t* bytes, int renumber, hipStream_t s) {
   // scratch: sorted stamps (pool u64), value ids in / out (pool u32 each), then the sort's own storage
   const size_t fixed = (size_t(pool) * 16 + 255) & ~size_t(255);
   size_t tmp = 0;
@@ -343,7 +346,7 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
   if (hipcub::DeviceRadixSort::SortPairsDescending(b + fixed, tmp, (const unsigned long long*)tag, keys_out, vin, vout, int(pool),
                                                    0, 64, s) != hipSuccess)
     return -1;
-  hipLaunchKernelGGL(xe_lru_link_kernel, dim3(blocks), dim3(256), 0, s, vout, cnt, link, hdr);
+  hipLaunchKernelGGL(xe_lru_link_kernel, dim3(blocks), dim3(256), 0, s, vout, cnt, link, hdr, tag, renumber);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -47,7 +47,7 @@ extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_b
 extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
-                                    size_t* bytes, hipStream_t s);
+                                    size_t* bytes, int renumber, hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -227,12 +227,13 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, siz
   return 0;
 }
 int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
-                      size_t* bytes, xe_stream_t) {  // xe_kernel.hip xe_launch_lru_relink
+                      size_t* bytes, int renumber, xe_stream_t) {  // xe_kernel.hip xe_launch_lru_relink
   if (!scratch) { *bytes = 8; return 0; }
   std::vector<uint32_t> v(pool);
   for (uint32_t i = 0; i < pool; i++) v[i] = i;
   std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return tag[a] > tag[b]; });
   for (uint32_t i = 0; i < cnt && i < pool; i++) {
+    if (renumber) tag[v[i]] = cnt - i;
     link[4 * uint64_t(v[i])] = i ? v[i - 1] : XE_NONE;
     link[4 * uint64_t(v[i]) + 1] = i + 1 < cnt ? v[i + 1] : XE_NONE;
   }
@@ -317,8 +318,8 @@ int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes
 }
 void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
-                      size_t* bytes, xe_stream_t s) {
-  return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, s);
+                      size_t* bytes, int renumber, xe_stream_t s) {
+  return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, renumber, s);
 }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
 int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
@@ -1064,16 +1065,28 @@ int map_upload(xe_vm* vm, HostMap& m) {
   return 0;
 }
 
-int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s) {
-  if (!m.links_stale || m.dkind != XE_DM_LRU) return 0;
+int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s, bool renumber = false) {
+  if ((!m.links_stale && !renumber) || m.dkind != XE_DM_LRU) return 0;
   uint64_t hdr[8];
   if (d2h(hdr, m.d_hdr, 64, s) || dsync(s)) return -1;
   size_t bytes = 0;
-  if (launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, nullptr, &bytes, s) ||
+  if (launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, nullptr, &bytes, 0, s) ||
       ensure_buf(&vm->d_relink, &vm->d_relink_cap, bytes) ||
-      launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, vm->d_relink, &bytes, s) || dsync(s))
+      launch_lru_relink(m.d_tag, m.pool_cap, uint32_t(hdr[2]), m.d_link, m.d_hdr, vm->d_relink, &bytes, renumber ? 1 : 0, s) ||
+      dsync(s))
     return -1;
   m.links_stale = false;
+  return 0;
+}
+
+// The 16-bit run epoch of the LRU stamps (xe_interp.h lru_stamp: epoch << 48) is about to wrap: rewrite
+// every map's stamps as their ranks in its UsageList (relinking first where only stamps are current), so
+// the next run can start again at epoch 1 and still sort after everything that came before.
+constexpr uint64_t kLruEpochMax = 0xffff;
+int lru_renumber(xe_vm* vm, xe_stream_t s) {
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].dkind == XE_DM_LRU && vm->maps[i].d_tag && lru_relink(vm, vm->maps[i], s, true)) return -1;
+  vm->lru_epoch = 0;
   return 0;
 }
 
@@ -1173,7 +1186,8 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
       if (!m.d_keys && dev_alloc((void**)&m.d_keys, rec.size() * 8)) return -1;
       if (h2d(m.d_keys, rec.data(), rec.size() * 8, st)) return -1;
       hdr[0] = n ? 0 : XE_NONE; hdr[1] = n ? n - 1 : XE_NONE; hdr[2] = n; hdr[3] = n;
-      hdr[5] = vm->lru_epoch << 40;  // the stamp base of the run in progress (xe_interp.h lru_stamp)
+      hdr[5] = vm->lru_epoch << 48;  // the stamp base of the run in progress (xe_interp.h lru_stamp)
+      hdr[6] = 0;
     } else {  // QUEUE / STACK: element i is Values[i]; the list starts at 0
       link.resize(pool);
       for (uint64_t i = 0; i < pool; i++) link[i] = uint32_t(i);
@@ -2329,9 +2343,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
   {
     bool lru = false;
     for (size_t i = 1; i < vm->maps.size(); i++) lru = lru || vm->maps[i].dkind == XE_DM_LRU;
-    const uint64_t e = lru ? (++vm->lru_epoch) << 40 : 0;
+    if (lru && vm->lru_epoch >= kLruEpochMax && lru_renumber(vm, s)) return fail(vm, XE_ERR_DEVICE, "LRU renumber");
+    const uint64_t e[2] = {lru ? (++vm->lru_epoch) << 48 : 0, 0};  // stamp base, one-lane touch counter
     for (size_t i = 1; i < vm->maps.size(); i++)
-      if (vm->maps[i].dkind == XE_DM_LRU && (h2d(vm->maps[i].d_hdr + 5, &e, 8, s) || dsync(s)))
+      if (vm->maps[i].dkind == XE_DM_LRU && (h2d(vm->maps[i].d_hdr + 5, e, 16, s) || dsync(s)))
         return fail(vm, XE_ERR_DEVICE, "LRU epoch");
   }
   if (P.trace && dmemset(vm->d_trace_cnt, 0, vm->trace_pk.size() * 4, s)) return fail(vm, XE_ERR_DEVICE, "trace reset");
@@ -3577,6 +3592,13 @@ int xe_debug_set_schedule(xe_vm* vm, uint32_t sched) {
   if (!vm) return XE_ERR_INVAL;
   if (int rc = xe_sync(vm)) return rc;
   vm->sched = sched;
+  return XE_OK;
+}
+
+int xe_debug_set_lru_epoch(xe_vm* vm, uint64_t epoch) {
+  if (!vm || epoch > kLruEpochMax) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  vm->lru_epoch = epoch;
   return XE_OK;
 }
 

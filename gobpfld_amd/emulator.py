@@ -327,6 +327,10 @@ class VM:
         """xe_debug_set_schedule: permute the chunk -> wave schedule of later parallel passes (0 = default)."""
         self._check(self.lib.debug_set_schedule(self.h, sched), "set schedule")
 
+    def set_lru_epoch(self, epoch: int) -> None:
+        """xe_debug_set_lru_epoch: the run counter of the LRU stamps (tests reach its renumbering)."""
+        self._check(self.lib.debug_set_lru_epoch(self.h, epoch), "set LRU epoch")
+
     def sync(self) -> None:
         """Complete every pipelined batch (in-order replays included)."""
         rc = self.lib.sync(self.h)

@@ -67,7 +67,7 @@ def default_workers() -> int:
 def code_object_name(src: str, arch: str = "gfx950", lib_path: str | os.PathLike | None = None) -> str:
     """File name of the code object `src` compiles to in a cache directory (no device needed)."""
     from . import _native as N
-    lib = N.Lib(lib_path or os.environ.get("XE_LIB", N.PRODUCT_LIB), "xe_")
+    lib = N.Lib(lib_path or N.product_path(), "xe_")
     buf = C.create_string_buffer(128)
     if lib.kernel_object_name(src.encode(), arch.encode(), buf, len(buf)) != 0:
         raise RuntimeError("xe_kernel_object_name failed")
@@ -86,7 +86,7 @@ def fill(sources, cache_dir: str | os.PathLike, arch: str = "gfx950", workers: i
         return []
     d = os.fspath(cache_dir)
     os.makedirs(d, exist_ok=True)
-    path = os.fspath(lib_path or os.environ.get("XE_LIB", N.PRODUCT_LIB))
+    path = os.fspath(lib_path or N.product_path())
     n = min(workers or default_workers(), len(uniq))
     with ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context("spawn"), initializer=_worker_init,
                              initargs=(path,)) as ex:

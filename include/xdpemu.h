@@ -417,6 +417,9 @@ int xe_reset_helper(xe_vm* vm, uint32_t id);
  * permutation of the 64-packet chunks). Results, register records and map contents may not depend on
  * it: the determinism tests run one batch under several schedules and compare. */
 int xe_debug_set_schedule(xe_vm* vm, uint32_t sched);
+/* Set the run counter the LRU stamps carry in their top 16 bits (xe_interp.h lru_stamp), so a test can
+ * reach the renumbering the runtime does before it wraps (0 <= epoch <= 0xffff) without 65,535 runs. */
+int xe_debug_set_lru_epoch(xe_vm* vm, uint64_t epoch);
 
 /* build / device info */
 const char* xe_version(void);

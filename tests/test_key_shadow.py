@@ -97,6 +97,12 @@ def k_alias(a):  # LDX makes R4 alias the stored object; the in-place add change
     a.add64(4, 1)
 
 
+def k_alias_ldimm(a):  # LD_IMM64 (src 0) assigns in place (inst_load.go:65): the aliased object takes it
+    k_wide(a)
+    a.ldx(8, 4, 10, -16)
+    a.ld_imm64(4, 0x1122334455667788)
+
+
 def k_alias_replaced(a):  # ADD of a pointer replaces R4 instead (inst_add.go:82-98): the object stays
     k_wide(a)
     a.ldx(4, 4, 10, -16)
@@ -140,6 +146,7 @@ CASES = {
     "straddle": (k_straddle, 1, 16, False, lambda p: p[0:4] + p[8:12] + p[8:16]),
     "overwrite": (k_overwrite, 1, 16, False, lambda p: p[0:4] + p[0:4] + p[8:16]),
     "alias": (k_alias, 1, 16, True, lambda p: ((int.from_bytes(p[0:8], "little") + 1) % 2**64).to_bytes(8, "little") + p[8:16]),
+    "alias_ldimm": (k_alias_ldimm, 1, 16, True, lambda p: (0x1122334455667788).to_bytes(8, "little") + p[8:16]),
     "alias_replaced": (k_alias_replaced, 1, 16, False, lambda p: p[0:16]),
     "unwritten": (k_unwritten, 1, 16, False, lambda p: p[0:12] + b"\0\0\0\0"),
     "two_preds": (k_two_preds, 1, 16, False, lambda p: p[0:16]),

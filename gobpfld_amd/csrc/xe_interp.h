@@ -3218,13 +3218,18 @@ XE_DEV void keyed_dset_item(const XeKeyed& K, uint32_t i) {
   }
 }
 XE_DEV uint32_t keyed_root(const XeKeyed& K, uint32_t x) {
-  // parents only decrease (keyed_union_item hooks under the smaller root), so the walk ends
+  // parents only decrease (keyed_union_item hooks under the smaller root), so the walk ends within dcap
+  // hops at a node that is its own parent. A parent outside D or a walk that does not end means the D
+  // table is not what the build wrote: the batch goes to the in-order replay (err bit 16, any err bit
+  // rolls the keyed path back) instead of forming chains from a partial root.
 #pragma unroll 1
   for (uint32_t hop = 0; hop < K.dcap; hop++) {
     const uint32_t p = xe_load_relaxed32(K.dcomp + x);
-    if (p == x || p >= K.dcap) return x;
+    if (p == x) return x;
+    if (p >= K.dcap) break;
     x = p;
   }
+  xe_atomic_or32(K.err, 16u);
   return x;
 }
 // hook every root of packet i's D keys under the smallest (parents only decrease: rounds converge)

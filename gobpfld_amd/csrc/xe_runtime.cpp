@@ -216,6 +216,14 @@ int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t
     return 0;
   }
   for (uint32_t i = 0; i < items; i++) keyed_step(*K, maps, skip, step, i);  // xe_kernel.hip xe_keyed_kernel
+  if (step == XE_KS_DSET && getenv("XE_HOSTSIM_DCYCLE")) {
+    // test-only fault injection: a parent cycle between D's first two keys, the state a corrupted D table
+    // leaves — keyed_root must send the batch to the replay instead of returning a partial root
+    uint32_t a = K->dcap, b = K->dcap;
+    for (uint32_t x = 0; x < K->dcap && b == K->dcap; x++)
+      if (K->dkid[x]) (a == K->dcap ? a : b) = x;
+    if (b != K->dcap) { K->dcomp[a] = b; K->dcomp[b] = a; }
+  }
   return 0;
 }
 int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
@@ -2567,7 +2575,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       vm->keyed_dnext = dmax;
       if (dcap < dmax) { keyed_trace("D full"); return krollback() ? -1 : 2; }
     }
-    if (small[XE_KS_ERR]) { keyed_trace("key log overflow"); return krollback() ? -1 : 1; }  // key log overflow
+    // key log overflow (1), a root walk that did not end (16): the in-order replay
+    if (small[XE_KS_ERR]) { keyed_trace(small[XE_KS_ERR] & 16u ? "root walk" : "key log overflow"); return krollback() ? -1 : 1; }
     {
       uint64_t nd = 0;
       for (uint32_t i = 0; i < 64; i++) nd += small[XE_KS_DCOUNT + i];

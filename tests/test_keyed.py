@@ -215,6 +215,16 @@ def test_keyed_escape_hostsim(oracle_lib, hostsim_lib):
     _check(hostsim_lib, oracle_lib, prog_escape(), maps, None, umem, descs, MODE_SEQUENTIAL, "escape")
 
 
+def test_keyed_root_cycle_replays_hostsim(oracle_lib, hostsim_lib, monkeypatch):
+    """A D table whose parents form a cycle (injected after the D step: XE_HOSTSIM_DCYCLE, host-simulation
+    build only) must not give chains from a partial root: keyed_root flags it and the batch replays in
+    order, exact."""
+    monkeypatch.setenv("XE_HOSTSIM_DCYCLE", "1")
+    prog, maps, entries = CASES["two_keys"]()
+    umem, descs = packets(3000, 64, seed=21)
+    _check(hostsim_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_SEQUENTIAL, "root cycle")
+
+
 def test_c3learn_hostsim(oracle_lib, hostsim_lib):
     prog, maps, entries, umem, descs = config_case("c3learn", 8192, flows_cap=4096)
     _check(hostsim_lib, oracle_lib, prog, maps, entries, umem, descs, MODE_KEYED, "c3learn")

@@ -275,6 +275,15 @@ def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536, nam
     return out
 
 
+def _rccl_version() -> str | None:
+    try:
+        import torch
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - informational only
+        return None
+
+
 def relaunch_ranks(gpus: int) -> int:
     """`bench.py --gpus N` started without torchrun: the same one-process-per-GPU run the driver launches
     (python -m torch.distributed.run ... bench.py), started as a child before anything touches the GPU,
@@ -394,6 +403,14 @@ def verify(name: str, vm, start: int, n: int, runs: int, d_ver, dist, world: int
                     f"{world} shard(s) of the header-derived per-run effect", "check_s": round(time.perf_counter() - t0, 2)}
 
 
+def _dsync(dev) -> None:
+    """torch.cuda.synchronize on a GPU device; nothing on the CPU (the gloo tests drive run_epochs with
+    host-simulation VMs over CPU tensors)."""
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream, warmup: int, steps: int, pipelined=True):
     """Warm-up epoch, then the timed epoch: `steps` pipelined batches and (N > 1) the shard exchange (one
     RCCL all-reduce per map, or the in-order replay), all inside the timed region. Returns the timed
@@ -417,24 +434,24 @@ def run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream, wa
             sts = [sync_run() for _ in range(k)]
         t_x = time.perf_counter()
         if epoch is not None:
-            torch.cuda.synchronize(dev)
+            _dsync(dev)
             t_x = time.perf_counter()
             x = epoch.exchange([sync_run] * k)
             exchanges["exact_sum" if x["exact_sum"] else "replayed"] += 1
         return sts, t_x
 
     epoch_of(warmup)
-    torch.cuda.synchronize(dev)
+    _dsync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    _dsync(dev)
     t0 = time.perf_counter()
     sts, t_x = epoch_of(steps)
-    torch.cuda.synchronize(dev)
+    _dsync(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    _dsync(dev)
     t2 = time.perf_counter()
     t = torch.tensor([t2 - t0, t1 - t_x], dtype=torch.float64, device=dev)
     if world > 1:
@@ -442,35 +459,77 @@ def run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream, wa
     return sts, float(t[0].item()), float(t[1].item()), exchanges
 
 
-def c5_side(args, rank: int, world: int, dev, stream, dist) -> dict:
-    """BASELINE configs[4] beside the default line: 33,554,432 C5 packets per GPU (per-flow HASH counters
-    {pkts, bytes}, 1M flows), `--c5-steps` pipelined batches per rank, then the shard exchange of the
-    per-flow deltas — one RCCL all-reduce of the value region — timed separately; verified like the main
-    line (every rank's per-flow counters against the header truth summed over all shards)."""
+def device_batch(name: str, start: int, n: int, dev):
+    """The batch of packets [start, start + n) resident in HBM: (d_umem, d_desc, descs). Fixed-size packets
+    back to back (C4's 16,777,216 x 1500 B = 25 GB) are laid out on the device — zeroed UMEM, then the
+    64-byte header rows copied into their packets' first bytes — instead of building the UMEM on the host
+    (the same bytes as workloads.build_batch: bytes past the header window are zero)."""
+    import torch
+    from gobpfld_amd import workloads as W
+    from gobpfld_amd._native import np_dtypes
+    cfg = W.CONFIGS[name]
+    if isinstance(cfg["pkt"], int) and cfg["pkt"] >= 64 and not cfg.get("frame"):
+        size = int(cfg["pkt"])
+        idx = np.arange(start, start + n, dtype=np.uint64)
+        d_umem = torch.zeros(n * size, dtype=torch.uint8, device=dev)
+        d_umem.view(n, size)[:, :64].copy_(torch.from_numpy(W.headers(name, idx, 64)))
+        descs = np.zeros(n, dtype=np_dtypes()[0])
+        descs["addr"] = np.arange(n, dtype=np.int64) * size
+        descs["len"] = size
+    else:
+        umem, descs = W.build_batch(name, start, n)
+        d_umem = torch.from_numpy(umem).to(dev)
+        del umem
+    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    return d_umem, d_desc, descs
+
+
+def side_line(name: str, n: int, steps: int, rank: int, world: int, dev, stream, dist) -> dict:
+    """A BASELINE config beside the default line, timed and verified the way the main line is: `n`
+    packets per GPU, one warm-up batch, then `steps` pipelined batches per rank and (N > 1) the shard
+    exchange, timed separately; the kernel's roofline from the batches' HIP-event kernel times.
+      c5 = configs[4]: 33,554,432 x 64 B per GPU, per-flow HASH counters {pkts, bytes} (1M flows); the
+           exchange is one RCCL all-reduce of the per-flow deltas;
+      c4 = configs[3]: 16,777,216 x 1500 B per GPU, the ~200-insn JEQ/JGT ACL (the 1500 B half of the
+           metric); no map, so the exchange reconciles nothing."""
     import torch
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
     from gobpfld_amd.shard import ShardEpoch
-    n = args.c5_packets
     start = rank * n
-    umem, descs = W.build_batch("c5", start, n)
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
-    del umem
+    d_umem, d_desc, descs = device_batch(name, start, n, dev)
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
     vm = VM(Settings(device=dev.index or 0))
-    W.setup_vm(vm, "c5")
+    W.setup_vm(vm, name)
     epoch = ShardEpoch(vm, list(vm.map_defs), dist, device=dev, stream=stream) if world > 1 else None
     sts, elapsed, x_s, exchanges = run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, n, d_ver, stream,
-                                              1, args.c5_steps)
-    ver = verify("c5", vm, start, n, 1 + args.c5_steps, d_ver, dist, world, dev)
-    vbytes = vm.map_values_bytes(1)
+                                              1, steps)
+    ver = verify(name, vm, start, n, 1 + steps, d_ver, dist, world, dev)
+    vbytes = vm.map_values_bytes(1) if vm.map_defs else 0
     vm.close()
+    del d_umem, d_desc, d_ver
+    torch.cuda.empty_cache()
     kms = [st["kernel_ms"] for st in sts]
-    return {"workload": WORKLOADS["c5"], "packets_per_gpu": n, "n_gpus": world, "steps": args.c5_steps,
-            "value": round(n * world * args.c5_steps / elapsed / 1e6, 3), "unit": "Mpkt/s",
-            "ms_per_step": round(elapsed / args.c5_steps * 1e3, 4), "avg_kernel_ms": round(float(np.mean(kms)), 4),
+    k_s = float(np.mean(kms)) / 1e3
+    sizes = descs["len"].astype(np.int64)
+    alg = float(alg_bytes_per_packet(name, sizes).sum())
+    traffic, traffic_src = pmc_traffic(name, n)
+    full = float((16 + sizes + 4).sum())  # SURVEY §8d: the full-packet variant for 1500 B packets
+    roof = {"bound": "hbm", "achieved": round(alg / k_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / k_s / 1e9 / HBM_PEAK_GBS, 5), "traffic": None if traffic is None else int(traffic),
+            "traffic_source": traffic_src, "kernel": "xe_jit_kernel", "avg_kernel_ms": round(k_s * 1e3, 4),
+            "alg_bytes_per_launch": int(alg), "alg_bytes_per_packet": "16 desc + min(len,64) header + 4 verdict",
+            **sq_issue(name, n, k_s)}
+    if name == "c4":
+        roof["full_packet_bytes_per_launch"] = int(full)
+        roof["full_packet_frac"] = round(full / k_s / 1e9 / HBM_PEAK_GBS, 5)
+    return {"workload": WORKLOADS[name], "packets_per_gpu": n, "n_gpus": world, "steps": steps,
+            "value": round(n * world * steps / elapsed / 1e6, 3), "unit": "Mpkt/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "avg_kernel_ms": round(k_s * 1e3, 4),
+            "roofline": roof,
             "exchange_ms": round(x_s * 1e3, 4) if world > 1 else None,
             "exchange": dict(exchanges, delta_bytes_per_gpu=vbytes, per="epoch of the timed steps") if world > 1 else None,
             "mode": sorted({st["mode_used"] for st in sts}), **ver}
@@ -489,6 +548,9 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     ap.add_argument("--no-ordered", action="store_true", help="skip the C2-RMW ordered-path lines (C2 only)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 side line (C2 only)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 (1500 B) side line (C2 only)")
+    ap.add_argument("--c4-packets", type=int, default=16 * 1024 * 1024, help="C4 side line: packets per GPU")
+    ap.add_argument("--c4-steps", type=int, default=10)
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run self-check")
     ap.add_argument("--c5-packets", type=int, default=32 * 1024 * 1024, help="C5 side line: packets per GPU")
     ap.add_argument("--c5-steps", type=int, default=8)
@@ -566,14 +628,25 @@ def main() -> None:
     if rank == 0 and not args.no_e2e:
         e2e = e2e_baseline(vm, umem, descs)
     del umem
-    c5 = None
+    c5 = c4 = None
     if name == "c2" and not args.no_c5:
-        c5 = c5_side(args, rank, world, dev, stream, dist)
+        c5 = side_line("c5", args.c5_packets, args.c5_steps, rank, world, dev, stream, dist)
+    if name == "c2" and not args.no_c4:
+        c4 = side_line("c4", args.c4_packets, args.c4_steps, rank, world, dev, stream, dist)
     ordered = None
     if rank == 0 and name == "c2" and not args.no_ordered:
         ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
         ordered["keyed_c3learn"] = keyed_paths(dev, stream, args.keyed_packets)
         ordered["keyed_c3lru"] = keyed_paths(dev, stream, args.keyed_packets, name="c3lru")
+    # what the exchange ran over: the process group's backend and the rank count it saw (N > 1), and
+    # RCCL's version; the C5 side line's per-flow delta exchange (time and bytes per GPU) beside it
+    comm = {"backend": dist.get_backend() if world > 1 else None,
+            "world": dist.get_world_size() if world > 1 else 1,
+            "rccl_version": _rccl_version(),
+            "c5_exchange_ms": c5["exchange_ms"] if c5 else None,
+            "c5_delta_bytes_per_gpu": (c5["exchange"] or {}).get("delta_bytes_per_gpu") if c5 else None,
+            "main_exchange_ms": round(x_s * 1e3, 4) if world > 1 else None,
+            "main_exchanges": dict(exchanges) if world > 1 else None}
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
@@ -615,7 +688,9 @@ def main() -> None:
                          **sq_issue(name, n, avg_kernel_s)},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "comm": comm,
             "c5": c5,
+            "c4": c4,
             "ordered": ordered,
         }
         print(json.dumps(out), flush=True)

@@ -56,3 +56,17 @@ def test_shard_truths_sum_over_ranks(oracle_lib):
     vm.run_batch(umem, descs)
     assert vm.map_dump(1) == B.expected_map("c2", tot)
     vm.close()
+
+
+def test_device_batch_layout_matches_host_batch():
+    """bench.device_batch lays fixed-size batches out on the device (C4: 25 GB of UMEM); the bytes and
+    descriptors must be workloads.build_batch's (checked here on a CPU tensor)."""
+    import torch
+    from gobpfld_amd import workloads as W
+    B = _bench()
+    for name in ("c4", "c2", "c3"):
+        d_umem, d_desc, descs = B.device_batch(name, 77, 1000, torch.device("cpu"))
+        umem, descs2 = W.build_batch(name, 77, 1000)
+        assert np.array_equal(d_umem.numpy(), umem), name
+        assert np.array_equal(descs, descs2), name
+        assert np.array_equal(d_desc.numpy(), descs2.view(np.uint8)), name

@@ -279,3 +279,58 @@ def test_two_rank_epoch_equals_single_vm(tmp_path, oracle_lib, built, name, n, c
         for r in range(world):
             assert (tmp_path / f"map{m}_r{r}.bin").read_bytes() == want, f"rank {r} map {m}"
     assert bool(np.load(tmp_path / "exact0.npy")[0]) == commutes
+
+
+def _rank_bench(rank, world, port, name, n, out_dir):
+    """bench.run_epochs itself (warm-up epoch + timed epoch, pipelined batches, the shard exchange inside
+    the timed region) on host-simulation VMs over CPU tensors."""
+    import importlib.util
+    import sys
+    sys.path.insert(0, ROOT)
+    from gobpfld_amd import _native as N
+    from gobpfld_amd.emulator import VM, Settings
+    from gobpfld_amd.shard import ShardEpoch
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = N.Lib(os.path.join(ROOT, "tests", "hostsim", "libxdpemu_hostsim.so"), "xe_")
+    vm = VM(Settings(), lib=lib)
+    _setup(vm, name, None)
+    shard = n // world
+    _batch.total = n
+    umem, descs = _batch(name, rank * shard, shard)
+    dev = torch.device("cpu")
+    d_umem = torch.from_numpy(umem.copy())
+    d_desc = torch.from_numpy(descs.view(np.uint8).copy())
+    d_ver = torch.zeros(shard, dtype=torch.int32)
+    epoch = ShardEpoch(vm, list(vm.map_defs), dist)
+    sts, elapsed, x_s, exchanges = B.run_epochs(vm, epoch, dist, world, dev, d_umem, d_desc, shard, d_ver, None, 1, 2)
+    np.save(os.path.join(out_dir, f"ver{rank}.npy"), d_ver.numpy().view(np.uint32))
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), np.array([exchanges["exact_sum"], exchanges["replayed"], len(sts)]))
+    for m in vm.map_defs:
+        with open(os.path.join(out_dir, f"map{m}_r{rank}.bin"), "wb") as f:
+            f.write(_dump(vm, m))
+    vm.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,n,replays", [("readvsadd", 256, True), ("c2", 8192, False)])
+def test_bench_run_epochs_two_ranks(tmp_path, oracle_lib, built, name, n, replays):
+    """The bench's own epoch loop at world size 2 (gloo): a read-vs-add program (rank 1's packets read the
+    counter rank 0's packets add to) must take the exchange's in-order replay branch in both epochs, C2
+    the exact delta sum; either way every rank ends with the oracle's single VM after 1 + 2 batches, and
+    the last verdicts are that VM's last run."""
+    world = 2
+    mp.start_processes(_rank_bench, args=(world, _free_port(), name, n, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    r3, dumps = _oracle(oracle_lib, name, n, None, steps=3)
+    ver = np.concatenate([np.load(tmp_path / f"ver{r}.npy") for r in range(world)])
+    assert (ver == r3.verdicts).all(), f"{name}: last verdicts differ from the single VM"
+    for m, want in dumps.items():
+        for r in range(world):
+            assert (tmp_path / f"map{m}_r{r}.bin").read_bytes() == want, f"rank {r} map {m}"
+    x = np.load(tmp_path / "x0.npy")
+    assert x[2] == 2, "two timed batches"
+    assert list(x[:2]) == ([0, 2] if replays else [2, 0]), x  # warm-up and timed epochs: replayed / exact sums

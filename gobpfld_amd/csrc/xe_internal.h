@@ -254,8 +254,9 @@ enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_
 #define XE_KS_LONG 67                       // some chain holds more than half the batch
 #define XE_KS_NCH 68                        // chains (the compacted chain list's length)
 #define XE_KS_CNEXT 69                      // the chain pass's work queue: next unclaimed chain
-#define XE_KS_CINS 128                      // [64 maps][XE_KSTRIPES] inserts the chains made
-#define XE_KS_WORDS (128 + 64 * XE_KSTRIPES)
+#define XE_KS_DINS 128                      // [64 maps] D keys some packet inserts (absent at the start)
+#define XE_KS_CINS 192                      // [64 maps][XE_KSTRIPES] inserts the chains made
+#define XE_KS_WORDS (192 + 64 * XE_KSTRIPES)
 #define XE_KEY_VALID 0x200ull               // dkey entry word 0: map index | nil-key 0x100 | valid | LRU value id << 32
 #define XE_KID_ARRAY_TAG 0xA7A7A7A700000000ull
 #define XE_KID_NIL_KEY 0x6e696c6b65790001ull  // the nil (empty) hash key
@@ -270,7 +271,8 @@ struct XeKeyed {
   uint32_t* cstart;    // [dcap] position of chain (root) c's first packet in order[]
   uint64_t* dkey;      // D table: [dcap * kw] a held-back insert's key (word 0: map | 0x100 nil | VALID)
   uint64_t* ikey;      // [n * XE_KINS * kw] the key words of a packet's held-back inserts (SPEC)
-  uint32_t* dcount;    // [64] D keys per map (HASH capacity bound)
+  uint32_t* dcount;    // [64] D keys per map (sizes the next batch's D table)
+  uint32_t* dins;      // [64] D keys per map that a packet inserts (the capacity bound: count + dins)
   uint32_t* cins;      // [64][XE_KSTRIPES] inserts made by the chains (added to the map counts after)
   uint32_t* err;       // build errors: 1 key log overflow, 2 no slot for a reservation, 8 D full
   uint32_t* changed;   // union-find round changed something

@@ -202,17 +202,23 @@ extern "C" __global__ void xe_keyed_kernel(XeKeyed K, const XeDevMap* maps, uint
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < items; i += uint64_t(gridDim.x) * blockDim.x)
     keyed_step(K, maps, skip, step, uint32_t(i));
 }
-// D keys per map (XE_KS_COUNT): a block histogram in LDS, one atomic per map per block
+// D keys per map (XE_KS_COUNT), and those of them a packet inserts (their first writer logged an
+// insert: the key words went with the D slot, XE_KEY_VALID): block histograms in LDS, one atomic per map
+// per block
 extern "C" __global__ void xe_keyed_count_kernel(XeKeyed K) {
-  __shared__ unsigned int hist[64];
-  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __shared__ unsigned int hist[64], ins[64];
+  if (threadIdx.x < 64) hist[threadIdx.x] = ins[threadIdx.x] = 0;
   __syncthreads();
   for (uint64_t x = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; x < K.dcap; x += uint64_t(gridDim.x) * blockDim.x) {
     const uint64_t kid = K.dkid[x];
-    if (kid) atomicAdd(&hist[kid >> 58], 1u);
+    if (kid) {
+      atomicAdd(&hist[kid >> 58], 1u);
+      if (K.dkey[x * K.kw] & XE_KEY_VALID) atomicAdd(&ins[kid >> 58], 1u);
+    }
   }
   __syncthreads();
   if (threadIdx.x < 64 && hist[threadIdx.x]) atomicAdd(K.dcount + threadIdx.x, hist[threadIdx.x]);
+  if (threadIdx.x < 64 && ins[threadIdx.x]) atomicAdd(K.dins + threadIdx.x, ins[threadIdx.x]);
 }
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s) {

@@ -212,7 +212,10 @@ int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* s
 int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items, xe_stream_t) {
   if (step == XE_KS_COUNT) {  // xe_kernel.hip xe_keyed_count_kernel
     for (uint32_t x = 0; x < K->dcap; x++)
-      if (K->dkid[x]) K->dcount[K->dkid[x] >> 58]++;
+      if (K->dkid[x]) {
+        K->dcount[K->dkid[x] >> 58]++;
+        if (K->dkey[uint64_t(x) * K->kw] & XE_KEY_VALID) K->dins[K->dkid[x] >> 58]++;
+      }
     return 0;
   }
   for (uint32_t i = 0; i < items; i++) keyed_step(*K, maps, skip, step, i);  // xe_kernel.hip xe_keyed_kernel
@@ -934,6 +937,7 @@ static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
     }
     vm->keyed_n = np;
     K.dcount = vm->d_ksmall + XE_KS_DCOUNT;
+    K.dins = vm->d_ksmall + XE_KS_DINS;
     K.err = vm->d_ksmall + XE_KS_ERR;
     K.changed = vm->d_ksmall + XE_KS_CHANGED;
     K.counts = vm->d_ksmall + XE_KS_NO;
@@ -2585,10 +2589,13 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       vm->keyed_dnext = uint32_t(next);
     }
     // a HASH insert can fail for capacity only in an order-dependent way (and an LRU insert would evict
-    // by the batch's order of touches): every key of D fits
+    // by the batch's order of touches): every key some packet inserts fits. Only an absent key's insert
+    // meets the capacity rule (maps_hash.go:84-89, maps_hash_lru.go:114-119) and nothing deletes in a
+    // keyed batch, so the bound is the live count + the D keys a packet inserts (XE_KS_DINS); keys
+    // that are only looked up, promoted or updated in place do not count
     for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];
-      const uint64_t nd = small[XE_KS_DCOUNT + i];
+      const uint64_t nd = small[XE_KS_DINS + i];
       if ((m.dkind != XE_DM_HASH && m.dkind != XE_DM_LRU) || !nd) continue;
       uint64_t cnt = 0;
       if (m.dkind == XE_DM_HASH) {

@@ -194,3 +194,22 @@ def test_packet_with_70000_touches(request, oracle_lib, which):
         assert (ra == rb).all()
         assert ua == ub
     assert [int.from_bytes(k, "little") for k in b[0][1]][:3] == [10, 6, 4]
+
+
+def test_lookups_past_capacity_stay_concurrent_hostsim(hostsim_lib, oracle_lib):
+    """A batch that only looks keys up (present and absent ones: 48 keys against MaxEntries 40 and 24
+    live) inserts nothing, so the keyed path's capacity bound (live + keys a packet inserts) holds and
+    the batch runs concurrently — it used to count every touched key and replay on one lane."""
+    rng = np.random.default_rng(5)
+    n = 4096
+    keys = rng.integers(0, KEYS, size=n).astype(np.uint32)
+    umem, descs = _batch(np.zeros(n, dtype=np.uint32), keys)
+    out = []
+    for lib in (hostsim_lib, oracle_lib):
+        vm, m = _vm(lib)
+        r = vm.run_batch(umem, descs)
+        out.append((r, vm.map_lru_order(m)))
+        vm.close()
+    (a, ua), (b, ub) = out
+    assert (a.results == b.results).all() and ua == ub
+    assert a.stats["mode_used"] != 2, a.stats

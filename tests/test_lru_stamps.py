@@ -31,7 +31,7 @@ def _program():
     a.ldx(4, 1, 6, 4).stx(4, 10, -4, 1)     # key -> fp-4
     a.st(4, 10, -8, 7)                      # value 7 -> fp-8
     a.ld_map(1, 1).mov64(2, src=10).add64(2, -4)
-    a.jmp(JNE, 7, "lookup", imm=0)
+    a.jmp(JEQ, 7, "lookup", imm=0)
     a.mov64(3, src=10).add64(3, -8).mov64(4, 0).call(2).exit()
     a.label("lookup").call(1)
     a.jmp(JEQ, 0, "miss", imm=0)

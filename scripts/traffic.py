@@ -73,7 +73,7 @@ def main() -> None:
             cal = fetch + 8 * n  # IMIX: descriptors stream; windows and probes at x1 (a lower bound)
         d["calibrated_estimate"] = {"hbm_bytes_per_packet": round((cal + write) / n, 1),
                                     "traffic_over_alg": round((cal + write) / alg, 3),
-                                    "model": "round-2 per-shape calibration of FETCH_SIZE (scripts/traffic_final.py)"}
+                                    "model": "round-2 per-shape calibration of FETCH_SIZE (profiles/r2/fetch_size_calibration*.json, applied by scripts/traffic.py main)"}
         (dst / f"{name}_traffic.json").write_text(json.dumps(d, indent=1) + "\n")
         print(name, "calibrated", d["calibrated_estimate"])
         print(name, d["per_packet"], "hbm/pkt", d["hbm_bytes_per_packet"], "ratio", d["traffic_over_alg"])

@@ -241,7 +241,7 @@ XE_HD uint64_t xe_kid(uint32_t m, uint64_t h) {
 // build steps (xe_interp.h keyed_step; items: packets, D slots, or insert-log entries)
 enum : uint32_t { XE_KS_DSET = 0, XE_KS_UNION, XE_KS_COMPRESS, XE_KS_ASSIGN, XE_KS_IOTA, XE_KS_NCHAIN, XE_KS_RESERVE,
                   XE_KS_COUNT, XE_KS_CSTART, XE_KS_CLONG, XE_KS_UNNEW, XE_KS_CFLAG, XE_KS_CLIST,
-                  XE_KS_LRUID };
+                  XE_KS_LRUID, XE_KS_FIRST, XE_KS_EKEY, XE_KS_EVICT, XE_KS_EMARK };
 // Same-address atomics serialise at the memory side, so nothing that many lanes do bumps one counter:
 // a new HASH key's words go to its D slot (whose CAS winner is unique), D keys per map are counted by
 // a per-block histogram over the D table, and the chains' inserts go to striped counters (by wave).
@@ -274,7 +274,8 @@ struct XeKeyed {
   uint32_t* dcount;    // [64] D keys per map (sizes the next batch's D table)
   uint32_t* dins;      // [64] D keys per map that a packet inserts (the capacity bound: count + dins)
   uint32_t* cins;      // [64][XE_KSTRIPES] inserts made by the chains (added to the map counts after)
-  uint32_t* err;       // build errors: 1 key log overflow, 2 no slot for a reservation, 8 D full
+  uint32_t* err;       // build errors: 1 key log overflow, 2 no slot for a reservation, 8 D full, 16 root walk,
+                       // 32 an eviction the batch's own packets could see
   uint32_t* changed;   // union-find round changed something
   uint32_t* ckey;      // [n] chain of packet i (dcap: none)
   uint32_t* okey;      // [n] sorted chain keys
@@ -284,6 +285,17 @@ struct XeKeyed {
   const uint8_t* skip; // [n] 1 = the packet runs on a chain (the parallel pass leaves it out)
   uint32_t n;          // packets of the batch
   uint32_t nO;         // packets on chains: order[0..nO) (a chain starts where the sorted key changes)
+  // LRU evictions in a keyed batch (xe_interp.h keyed_evict_item): the inserts of new keys, in packet
+  // order of their first insert, take the oldest live values of the batch's start as victims
+  uint32_t* dfirst;    // [dcap] first packet that inserts D key x (XE_NONE: none)
+  uint32_t* dvict;     // [dcap] the value id the insert of D key x evicts (XE_NONE: none)
+  uint64_t* ekey;      // [dcap] sort keys: map << 32 | dfirst of the LRU inserts, ~0 for anything else
+  uint64_t* ekey2;     // [dcap] sorted
+  uint32_t* eval;      // [dcap] D indices (sort values)
+  uint32_t* eval2;     // [dcap] D indices in (map, first insert) order
+  const uint64_t* etsnap;  // the evicting map's value stamps at the batch's start
+  const uint32_t* vorder;  // its value ids by start stamp, most recent first (the UsageList of the start)
+  uint32_t em, eoff, efree, ecnt0;  // map; its first sorted position; inserts before the first eviction; live count
 };
 
 // General lane model (xe_interp.h, XE_GEN): the Go object model without fixed limits, per lane in a

@@ -2115,9 +2115,9 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       if (int e = key_touch(L, P, kid, false)) return e;  // presence (and the count) are read
 #endif
     uint32_t v = lru_find(M, kw, empty);
-    if (v == XE_NONE && *map_hdr(M, 2) + 1 > M.max_entries) {
-      // an eviction depends on the whole batch's order of touches: the keyed schedule only runs when
-      // count + the batch's written keys fit MaxEntries (xe_runtime.cpp keyed), else the in-order replay
+    // keyed batches (XE_MODE_SPEC / XE_MODE_CHAIN) decide evictions in the build instead: SPEC logs the
+    // insert, a chain's insert deletes the victim the build gave it (keyed_evict_item)
+    if (v == XE_NONE && *map_hdr(M, 2) + 1 > M.max_entries && P.mode != XE_MODE_SPEC && P.mode != XE_MODE_CHAIN) {
       if (xe_concurrent(P)) return XE_EV_ORD;
       const uint32_t tail = uint32_t(*map_hdr(M, 1));
       if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
@@ -2149,11 +2149,22 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       return helper_errno_result(L, 0);
     }
     if (P.mode == XE_MODE_CHAIN && v == XE_NONE) {
+      // the first insert of the key must be the one the build ranked (XE_KS_FIRST: its victim, if any,
+      // was chosen by that rank)
+      const int64_t d = dset_find(P.K, kid);
+      if (d < 0) return XE_EV_ORD;
+      const uint32_t first = P.K.dfirst[d];
+      if (first != XE_NONE && first != L.pidx) return XE_EV_ORD;
       // the record reserved for this key holds its value id (xe_runtime.cpp keyed: XE_KS_LRUID, RESERVE)
       const int64_t slot = empty ? -1 : hash_claim(M, kw, false, P.K.cins + m * XE_KSTRIPES + (L.wave % XE_KSTRIPES));
       if (slot < 0) return XE_EV_ORD;  // the nil key (no reservation) or a key that left its chain
       v = lru_vid(M, slot);
       *lru_link(M, v, 2) = uint32_t(slot);
+      const uint32_t victim = P.K.dvict[d];
+      if (victim != XE_NONE) {  // delete, :163-183: out of the UsageList (stamp 0), its record a tombstone
+        ((XE_GP(uint64_t))M.tag)[victim] = 0;
+        ((XE_GP(uint64_t))M.keys)[uint64_t(*lru_link(M, victim, 2)) * M.rwords] = XE_SLOT_TOMB;
+      }
     }
 #endif
     if (v == XE_NONE) {
@@ -3300,6 +3311,64 @@ XE_DEV void keyed_lruid_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x)
   const uint32_t id = xe_wave_alloc_at(next, want);
   if (want) en[0] = (en[0] & 0xffffffffull) | (uint64_t(id) << 32);
 }
+// ---- LRU evictions in a keyed batch (maps_hash_lru.go:114-119: an insert into a full map first deletes
+// UsageList[len-1]). In packet order the UsageList's tail is the least recently used value that no packet
+// of the batch has touched yet, because every touch and insert moves a key to the head. When none of the
+// E oldest values of the batch's start is touched by any packet, the j-th evicting insert in packet order
+// (an insert of a new key is evicting once the live count has reached MaxEntries) deletes exactly the
+// j-th oldest of them: the build ranks the inserts of new keys by the packet that first inserts them,
+// the chains delete the victims at those inserts, and any packet that would see a victim — in SPEC
+// (its stamp moved, or its key is written) or in the chains (its key is now a D entry of no chain) —
+// sends the batch to the in-order replay.
+//   XE_KS_FIRST (packets): the first inserting packet of every D key
+XE_DEV void keyed_first_item(const XeKeyed& K, uint32_t i) {
+  const uint32_t n = K.kcnt[i];
+  if (n > XE_KLOG) return;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; j++) {
+    const uint64_t e = K.klog[uint64_t(i) * XE_KLOG + j];
+    if (!(e & XE_KLOG_INS)) continue;
+    const int64_t d = dset_find(K, e & ~XE_KLOG_FLAGS);
+    if (d >= 0) xe_atomic_min32(K.dfirst + d, i);
+  }
+}
+//   XE_KS_EKEY (D slots): sort keys map << 32 | first insert of the LRU inserts (everything else last)
+XE_DEV void keyed_ekey_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x) {
+  uint64_t key = ~0ull;
+  if (((XE_GP(const unsigned long long))K.dkid)[x]) {
+    const uint64_t en = K.dkey[uint64_t(x) * K.kw];
+    const uint32_t m = uint32_t(en & 0xffu);
+    if ((en & XE_KEY_VALID) && maps[m].kind == XE_DM_LRU) key = (uint64_t(m) << 32) | K.dfirst[x];
+  }
+  K.ekey[x] = key;
+  K.eval[x] = x;
+  K.dvict[x] = XE_NONE;
+}
+//   XE_KS_EVICT (the inserts of map em, i-th in packet order): the victim of the i-th insert
+XE_DEV void keyed_evict_item(const XeKeyed& K, const XeDevMap* maps, uint32_t i) {
+  const uint32_t d = K.eval2[K.eoff + i];
+  if (i < K.efree) return;  // the map still had room: no eviction
+  const uint32_t q = i - K.efree;
+  if (q >= K.ecnt0) { xe_atomic_or32(K.err, 32u); return; }  // it would evict a key this batch inserted
+  const uint32_t v = K.vorder[K.ecnt0 - 1 - q];
+  const XeDevMap& M = maps[K.em];
+  // touched by some packet: a SPEC lookup moved its stamp, or some packet writes its key
+  const bool moved = ((XE_GP(const uint64_t))M.tag)[v] != K.etsnap[v];
+  const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(v) + 2];
+  if (moved || dset_find(K, kid_slot(K.em, M, slot)) >= 0) { xe_atomic_or32(K.err, 32u); return; }
+  K.dvict[d] = v;
+}
+//   XE_KS_EMARK (the same items): each victim's key becomes a D entry of no chain, so a chain packet that
+//   would still look it up leaves its chain (key_touch) instead of seeing it present or deleted
+XE_DEV void keyed_emark_item(const XeKeyed& K, const XeDevMap* maps, uint32_t i) {
+  const uint32_t d = K.eval2[K.eoff + i];
+  const uint32_t v = K.dvict[d];
+  if (v == XE_NONE) return;
+  const XeDevMap& M = maps[K.em];
+  const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(v) + 2];
+  keyed_dset_insert(K, kid_slot(K.em, M, slot));
+}
+
 // D slot x, after the chains: the reservation of a new HASH key loses its "claimed in this launch" mark
 // (a chain's insert already turned it FULL; an unused one stays a plain tombstone holding its key), so a
 // later keyed batch's hash_reserve finds it by its key words instead of reserving another record
@@ -3359,6 +3428,10 @@ XE_DEV void keyed_step(const XeKeyed& K, const XeDevMap* maps, uint8_t* skip, ui
     case XE_KS_CFLAG: keyed_cflag_item(K, i); break;
     case XE_KS_CLIST: keyed_clist_item(K, i); break;
     case XE_KS_LRUID: keyed_lruid_item(K, maps, i); break;
+    case XE_KS_FIRST: keyed_first_item(K, i); break;
+    case XE_KS_EKEY: keyed_ekey_item(K, maps, i); break;
+    case XE_KS_EVICT: keyed_evict_item(K, maps, i); break;
+    case XE_KS_EMARK: keyed_emark_item(K, maps, i); break;
     default: break;
   }
 }

@@ -339,6 +339,7 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
   }
   if (*bytes < fixed + tmp || cnt > pool) return -1;
   if (!cnt || !pool) {
+    if (renumber == 2) return 0;  // nothing live: no order to give
     hipLaunchKernelGGL(xe_lru_empty_kernel, dim3(1), dim3(1), 0, s, hdr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -352,8 +353,24 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
   if (hipcub::DeviceRadixSort::SortPairsDescending(b + fixed, tmp, (const unsigned long long*)tag, keys_out, vin, vout, int(pool),
                                                    0, 64, s) != hipSuccess)
     return -1;
+  if (renumber == 2) return hipGetLastError() == hipSuccess ? 0 : -1;  // the order only (vout)
   hipLaunchKernelGGL(xe_lru_link_kernel, dim3(blocks), dim3(256), 0, s, vout, cnt, link, hdr, tag, renumber);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// keyed LRU evictions: the D table's LRU inserts sorted by (map, first inserting packet)
+extern "C" int xe_launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, hipStream_t s) {
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                         (const uint32_t*)nullptr, (uint32_t*)nullptr, int(K->dcap), 0, 64, s) != hipSuccess)
+    return -1;
+  if (!scratch) {
+    *bytes = tmp;
+    return 0;
+  }
+  if (*bytes < tmp) return -1;
+  return hipcub::DeviceRadixSort::SortPairs(scratch, tmp, (const unsigned long long*)K->ekey, (unsigned long long*)K->ekey2,
+                                            K->eval, K->eval2, int(K->dcap), 0, 64, s) == hipSuccess ? 0 : -1;
 }
 
 // host-side launchers (called from xe_runtime.cpp)

@@ -44,6 +44,7 @@ extern "C" void* xe_jit_get(const XeUop* const* progs, const uint32_t* lens, uin
 extern "C" int xe_launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items,
                                hipStream_t s);
 extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
@@ -237,12 +238,24 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t, void* scratch, siz
   for (uint32_t i = 0; i < n; i++) { K->okey[i] = v[i].first; K->order[i] = v[i].second; }
   return 0;
 }
+int launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, xe_stream_t) {  // xe_launch_keyed_esort
+  if (!scratch) { *bytes = 8; return 0; }
+  std::vector<std::pair<uint64_t, uint32_t>> v(K->dcap);
+  for (uint32_t i = 0; i < K->dcap; i++) v[i] = {K->ekey[i], K->eval[i]};
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  for (uint32_t i = 0; i < K->dcap; i++) { K->ekey2[i] = v[i].first; K->eval2[i] = v[i].second; }
+  return 0;
+}
 int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                       size_t* bytes, int renumber, xe_stream_t) {  // xe_kernel.hip xe_launch_lru_relink
-  if (!scratch) { *bytes = 8; return 0; }
+  // scratch as on the device: sorted stamps, value ids in, value ids out (lru_sorted_ids)
+  if (!scratch) { *bytes = size_t(pool) * 16 + 256; return 0; }
   std::vector<uint32_t> v(pool);
   for (uint32_t i = 0; i < pool; i++) v[i] = i;
   std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return tag[a] > tag[b]; });
+  uint32_t* vout = (uint32_t*)((uint8_t*)scratch + size_t(pool) * 8) + pool;
+  for (uint32_t i = 0; i < pool; i++) vout[i] = v[i];
+  if (renumber == 2) return 0;  // the order only
   for (uint32_t i = 0; i < cnt && i < pool; i++) {
     if (renumber) tag[v[i]] = cnt - i;
     link[4 * uint64_t(v[i])] = i ? v[i - 1] : XE_NONE;
@@ -317,6 +330,9 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
 int host_alloc(void** p, size_t n) { return hipHostMalloc(p, n ? n : 8, hipHostMallocDefault) == hipSuccess ? 0 : -1; }
 int launch_keyed(const XeKeyed* K, const XeDevMap* maps, uint8_t* skip, uint32_t step, uint32_t items, xe_stream_t s) {
   return xe_launch_keyed(K, maps, skip, step, items, s);
+}
+int launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, xe_stream_t s) {
+  return xe_launch_keyed_esort(K, scratch, bytes, s);
 }
 int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
   return xe_launch_keyed_sort(K, n, end_bit, scratch, bytes, s);
@@ -904,6 +920,7 @@ static void keyed_free(xe_vm* vm) {
   XeKeyed& K = vm->kd;
   dev_free(K.klog); dev_free(K.kcnt); dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.ikey);
   dev_free(K.cstart);
+  dev_free(K.dfirst); dev_free(K.dvict); dev_free(K.ekey); dev_free(K.ekey2); dev_free(K.eval); dev_free(K.eval2);
   dev_free(K.ckey); dev_free(K.okey); dev_free(K.order); dev_free(K.iota);
   dev_free(vm->d_skip); dev_free(vm->d_ksmall); dev_free(vm->d_ksort);
   K = XeKeyed{};
@@ -945,10 +962,15 @@ static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
   }
   if (vm->keyed_dcap != dcap || vm->keyed_kw < kw) {
     dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.cstart);
+    dev_free(K.dfirst); dev_free(K.dvict); dev_free(K.ekey); dev_free(K.ekey2); dev_free(K.eval); dev_free(K.eval2);
     K.dkey = nullptr; K.dkid = nullptr; K.dcomp = K.cstart = nullptr;
+    K.dfirst = K.dvict = K.eval = K.eval2 = nullptr; K.ekey = K.ekey2 = nullptr;
     vm->keyed_dcap = 0;
     if (dev_alloc((void**)&K.dkey, uint64_t(dcap) * kw * 8) || dev_alloc((void**)&K.dkid, uint64_t(dcap) * 8) ||
-        dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4) || dev_alloc((void**)&K.cstart, uint64_t(dcap) * 4)) {
+        dev_alloc((void**)&K.dcomp, uint64_t(dcap) * 4) || dev_alloc((void**)&K.cstart, uint64_t(dcap) * 4) ||
+        dev_alloc((void**)&K.dfirst, uint64_t(dcap) * 4) || dev_alloc((void**)&K.dvict, uint64_t(dcap) * 4) ||
+        dev_alloc((void**)&K.ekey, uint64_t(dcap) * 8) || dev_alloc((void**)&K.ekey2, uint64_t(dcap) * 8) ||
+        dev_alloc((void**)&K.eval, uint64_t(dcap) * 4) || dev_alloc((void**)&K.eval2, uint64_t(dcap) * 4)) {
       keyed_free(vm);
       return -1;
     }
@@ -1089,6 +1111,12 @@ int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s, bool renumber = false) {
     return -1;
   m.links_stale = false;
   return 0;
+}
+
+// where launch_lru_relink leaves the pool's value ids sorted by stamp, most recent first (its scratch:
+// sorted stamps, ids in, ids out)
+const uint32_t* lru_sorted_ids(const void* scratch, uint32_t pool) {
+  return (const uint32_t*)((const uint8_t*)scratch + size_t(pool) * 8) + pool;
 }
 
 // The 16-bit run epoch of the LRU stamps (xe_interp.h lru_stamp: epoch << 48) is about to wrap: rewrite
@@ -2532,7 +2560,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     };
     XeKeyed K = vm->kd;
     K.n = n;
-    if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, XE_KS_WORDS * 4, s))
+    if (dmemset(K.dkid, 0, uint64_t(K.dcap) * 8, s) || dmemset(vm->d_ksmall, 0, XE_KS_WORDS * 4, s) ||
+        dmemset(K.dfirst, 0xff, uint64_t(K.dcap) * 4, s) || dmemset(K.dvict, 0xff, uint64_t(K.dcap) * 4, s))
       return fail(vm, XE_ERR_DEVICE, "keyed reset");
     const uint32_t grid = parallel_grid(vm, kjit, general, n, P.nmaps);
     XeParams X = P;
@@ -2588,6 +2617,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       while (next < 4 * nd && next < dmax) next <<= 1;
       vm->keyed_dnext = uint32_t(next);
     }
+    std::map<size_t, uint64_t> evict;  // LRU map -> the evictions its inserts make
     // a HASH insert can fail for capacity only in an order-dependent way (and an LRU insert would evict
     // by the batch's order of touches): every key some packet inserts fits. Only an absent key's insert
     // meets the capacity rule (maps_hash.go:84-89, maps_hash_lru.go:114-119) and nothing deletes in a
@@ -2614,7 +2644,49 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
           return 2;
         }
       }
-      if (cnt + nd > m.def.max_entries) { keyed_trace("capacity"); return krollback() ? -1 : 1; }
+      if (cnt + nd > m.def.max_entries) {
+        if (m.dkind != XE_DM_LRU) { keyed_trace("capacity"); return krollback() ? -1 : 1; }
+        evict[i] = cnt + nd - m.def.max_entries;  // the batch's inserts evict: planned below
+      }
+    }
+    // LRU evictions (xe_interp.h keyed_evict_item): rank every LRU map's new keys by their first
+    // inserting packet, give the inserts past the map's room the oldest values of the batch's start as
+    // victims, and replay in order if any packet of the batch touches one of them
+    if (!evict.empty()) {
+      size_t eb = 0;
+      if (step(XE_KS_FIRST, n) || step(XE_KS_EKEY, K.dcap) || launch_keyed_esort(&K, nullptr, &eb, s) ||
+          ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, eb) || launch_keyed_esort(&K, vm->d_ksort, &eb, s))
+        return fail(vm, XE_ERR_DEVICE, "keyed evictions");
+      uint64_t off = 0;
+      for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
+        HostMap& m = vm->maps[i];
+        if (m.dkind != XE_DM_LRU) continue;
+        const uint32_t nd = small[XE_KS_DINS + i];
+        if (evict.count(i)) {
+          const uint64_t cnt = kh0[i * 8 + 2];
+          // the start's UsageList by stamp (the stamps at the batch's start: the snapshot of ordered_hdr_read)
+          size_t rb = 0;
+          if (launch_lru_relink(m.d_tsnap, m.pool_cap, uint32_t(cnt), m.d_link, m.d_hdr, nullptr, &rb, 2, s) ||
+              ensure_buf(&vm->d_relink, &vm->d_relink_cap, rb) ||
+              launch_lru_relink(m.d_tsnap, m.pool_cap, uint32_t(cnt), m.d_link, m.d_hdr, vm->d_relink, &rb, 2, s))
+            return fail(vm, XE_ERR_DEVICE, "keyed evictions (order)");
+          K.em = uint32_t(i);
+          K.eoff = uint32_t(off);
+          K.efree = uint32_t(m.def.max_entries - cnt);
+          K.ecnt0 = uint32_t(cnt);
+          K.etsnap = m.d_tsnap;
+          K.vorder = lru_sorted_ids(vm->d_relink, m.pool_cap);
+          if (step(XE_KS_EVICT, nd) || step(XE_KS_EMARK, nd)) return fail(vm, XE_ERR_DEVICE, "keyed evictions");
+        }
+        off += nd;
+      }
+      if (read_small()) return fail(vm, XE_ERR_DEVICE, "keyed evictions");
+      if (small[XE_KS_ERR] & 8u) {  // the victims' keys did not fit the D table
+        vm->keyed_dnext = dmax;
+        if (dcap < dmax) { keyed_trace("D full (victims)"); return krollback() ? -1 : 2; }
+      }
+      if (small[XE_KS_ERR]) { keyed_trace("eviction seen by the batch"); return krollback() ? -1 : 1; }
+      K.em = 0;
     }
     uint32_t end_bit = 1;
     while ((1ull << end_bit) <= K.dcap) end_bit++;
@@ -2658,7 +2730,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (klaunch(&X, cgrid) || step(XE_KS_UNNEW, K.dcap)) return fail(vm, XE_ERR_DEVICE, "kernel launch (keyed chains)");
     if (read_aux() || read_small()) return fail(vm, XE_ERR_DEVICE, "kernel failed (keyed chains)");
     if (run_conflict(red, P.nmaps)) { keyed_trace("chain conflict"); return rollback(true) ? -1 : 1; }  // a packet left its chain / an order-dependent add
-    // the chains' inserts into the map counts (LRU_HASH: header word 2)
+    // the chains' inserts into the map counts (LRU_HASH: header word 2, less its evictions). An LRU map
+    // with evictions must have seen every ranked insert: one that did not happen shifts the victims of
+    // the inserts after it
+    for (const auto& [i, ev] : evict) {
+      uint32_t add = 0;
+      for (uint32_t k = 0; k < XE_KSTRIPES; k++) add += small[XE_KS_CINS + i * XE_KSTRIPES + k];
+      if (add != small[XE_KS_DINS + i]) { keyed_trace("eviction ranks"); return rollback(true) ? -1 : 1; }
+    }
     for (size_t i = 1; i < vm->maps.size() && i < 64; i++) {
       HostMap& m = vm->maps[i];
       uint32_t add = 0;
@@ -2673,6 +2752,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         uint64_t cnt = 0;
         if (d2h(&cnt, m.d_hdr + 2, 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
         cnt += add;
+        if (evict.count(i)) cnt -= evict[i];
         if (h2d(m.d_hdr + 2, &cnt, 8, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "count");
       }
     }

@@ -1,0 +1,123 @@
+"""LRU evictions in a keyed batch (xe_interp.h keyed_evict_item; reference: emulator/maps_hash_lru.go:93-161,
+eviction at :114-119, delete at :163-183).
+
+A learning batch into a full LRU_HASH map evicts: in packet order the j-th insert of a new key past the
+map's room deletes the UsageList's tail at that moment. When no packet of the batch touches the E oldest
+values of the batch's start, that tail is the j-th oldest of them, so the device runs the batch on the
+keyed path (mode KEYED) with those victims; when some packet looks one of them up, or writes it, the
+batch must replay in order (mode SEQUENTIAL). Either way results, the UsageList and the entries equal
+the oracle's sequential VM."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from gobpfld_amd.emulator import MAP_LRU_HASH, MODE_KEYED, MODE_SEQUENTIAL, MapDef, Settings
+
+MAX = 64
+
+
+def _program():
+    """packet = [op u32][key u32]: op 0 looks the key up (R0 = value or 0xFFFF), op 1 updates it to 7
+    (R0 = the helper's result)."""
+    from gobpfld_amd.asm import JEQ, Asm
+    a = Asm()
+    a.ldx(4, 6, 1, 0)
+    a.ldx(4, 7, 6, 0)
+    a.ldx(4, 1, 6, 4).stx(4, 10, -4, 1)
+    a.st(4, 10, -8, 7)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4)
+    a.jmp(JEQ, 7, "lookup", imm=0)
+    a.mov64(3, src=10).add64(3, -8).mov64(4, 0).call(2).exit()
+    a.label("lookup").call(1)
+    a.jmp(JEQ, 0, "miss", imm=0)
+    a.ldx(4, 0, 0, 0).exit()
+    a.label("miss").mov64(0, 0xFFFF).exit()
+    return a.assemble()
+
+
+def _batch(ops, keys):
+    from gobpfld_amd._native import np_dtypes
+    n = len(keys)
+    pk = np.zeros((n, 2), dtype="<u4")
+    pk[:, 0] = ops
+    pk[:, 1] = keys
+    descs = np.zeros(n, dtype=np_dtypes()[0])
+    descs["addr"] = np.arange(n) * 8
+    descs["len"] = 8
+    return pk.view(np.uint8).reshape(-1).copy(), descs
+
+
+def _vm(lib, live):
+    from gobpfld_amd.emulator import VM
+    vm = VM(Settings(), lib=lib)
+    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 4, MAX))
+    for k in range(live):  # key k updated k-th: key 0 is the oldest
+        vm.map_update(m, int(k).to_bytes(4, "little"), int(1000 + k).to_bytes(4, "little"))
+    vm.set_entrypoint(vm.add_raw_program(_program()))
+    return vm, m
+
+
+def _learning_batch(n, seed, touch_oldest=False, live=MAX):
+    """Lookups and updates of the newest half of the live keys, and inserts of new keys 1000+ (each new
+    key inserted by several packets); with touch_oldest, one packet looks up the oldest key."""
+    rng = np.random.default_rng(seed)
+    ops = (rng.random(n) < 0.5).astype(np.uint32)
+    keys = rng.integers(live // 2, live, size=n).astype(np.uint32)
+    new = rng.random(n) < 0.3
+    ops[new] = 1
+    keys[new] = 1000 + rng.integers(0, max(1, n // 20), size=int(new.sum()))
+    if touch_oldest:
+        ops[n // 2], keys[n // 2] = 0, 0
+    return _batch(ops, keys)
+
+
+def _run(lib, batches, live=MAX):
+    vm, m = _vm(lib, live)
+    out = []
+    for umem, descs in batches:
+        r = vm.run_batch(umem, descs)
+        keys, vals = vm.map_dump(m)
+        out.append((r.results.copy(), r.stats["mode_used"], vm.map_lru_order(m), bytes(np.asarray(keys)), bytes(np.asarray(vals))))
+    vm.close()
+    return out
+
+
+def _check(got, want, modes):
+    for i, ((ra, ma, ua, ka, va), (rb, _, ub, kb, vb)) in enumerate(zip(got, want)):
+        assert (ra == rb).all(), f"batch {i}: results differ"
+        assert ua == ub, f"batch {i}: UsageList differs"
+        assert ka == kb and va == vb, f"batch {i}: entries differ"
+        if modes[i] is not None:
+            assert ma == modes[i], f"batch {i}: mode {ma}, want {modes[i]}"
+
+
+CASES = {
+    # full map, inserts past its room: the oldest values go, in the order of their inserts
+    "evicting": (lambda: [_learning_batch(400, 1)], [MODE_KEYED]),
+    # two batches in a row on one VM (the second evicts the first's survivors in stamp order)
+    "two_batches": (lambda: [_learning_batch(300, 2), _learning_batch(300, 3)], [MODE_KEYED, MODE_KEYED]),
+    # a packet looks a victim up: the batch replays in order
+    "victim_touched": (lambda: [_learning_batch(400, 4, touch_oldest=True)], [MODE_SEQUENTIAL]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_lru_evictions_hostsim(hostsim_lib, oracle_lib, case):
+    make, modes = CASES[case]
+    batches = make()
+    _check(_run(hostsim_lib, batches), _run(oracle_lib, batches), modes)
+
+
+def test_lru_room_then_evictions_hostsim(hostsim_lib, oracle_lib):
+    """A map with room for some of the batch's new keys: the first inserts fill it, the rest evict."""
+    batches = [_learning_batch(400, 5, live=MAX - 10)]
+    _check(_run(hostsim_lib, batches, live=MAX - 10), _run(oracle_lib, batches, live=MAX - 10), [MODE_KEYED])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_lru_evictions_device(gpu_lib, oracle_lib, case):
+    make, modes = CASES[case]
+    batches = make()
+    _check(_run(gpu_lib, batches), _run(oracle_lib, batches), modes)

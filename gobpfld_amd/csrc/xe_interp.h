@@ -2159,12 +2159,14 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       const int64_t slot = empty ? -1 : hash_claim(M, kw, false, P.K.cins + m * XE_KSTRIPES + (L.wave % XE_KSTRIPES));
       if (slot < 0) return XE_EV_ORD;  // the nil key (no reservation) or a key that left its chain
       v = lru_vid(M, slot);
-      *lru_link(M, v, 2) = uint32_t(slot);
       const uint32_t victim = P.K.dvict[d];
-      if (victim != XE_NONE) {  // delete, :163-183: out of the UsageList (stamp 0), its record a tombstone
+      if (victim != XE_NONE) {
+        // delete, :163-183: out of the UsageList (stamp 0), its record a tombstone; the new key's value id
+        // is the victim's (keyed_lruid_item), whose pool entry it overwrites below
         ((XE_GP(uint64_t))M.tag)[victim] = 0;
         ((XE_GP(uint64_t))M.keys)[uint64_t(*lru_link(M, victim, 2)) * M.rwords] = XE_SLOT_TOMB;
       }
+      *lru_link(M, v, 2) = uint32_t(slot);
     }
 #endif
     if (v == XE_NONE) {
@@ -3299,17 +3301,21 @@ XE_DEV void keyed_reserve_item(const XeKeyed& K, const XeDevMap* maps, uint32_t 
 }
 // D slot x: a new LRU key gets a value id from its map's pool (next id, hdr[3]); lanes taking ids from
 // the same map share one atomic per wave. Every lane of the launch calls this (no early exit).
+// An insert that evicts (keyed_evict_item) takes over its victim's value id instead: no packet of the
+// batch holds a pointer to the victim's value (none touches it), so the pool does not grow by evictions.
 XE_DEV void keyed_lruid_item(const XeKeyed& K, const XeDevMap* maps, uint32_t x) {
   bool want = false;
-  uint32_t m = 0;
+  uint32_t m = 0, victim = XE_NONE;
   XE_GP(uint64_t) en = (XE_GP(uint64_t))K.dkey + uint64_t(x) * K.kw;
   if (((XE_GP(const unsigned long long))K.dkid)[x] && (en[0] & XE_KEY_VALID) && !(en[0] & 0x100ull)) {
     m = uint32_t(en[0] & 0xffu);
     want = maps[m].kind == XE_DM_LRU;
+    victim = want ? K.dvict[x] : XE_NONE;
   }
-  unsigned int* next = want ? (unsigned int*)maps[m].hdr + 6 : (unsigned int*)K.err;  // hdr[3], low word
-  const uint32_t id = xe_wave_alloc_at(next, want);
-  if (want) en[0] = (en[0] & 0xffffffffull) | (uint64_t(id) << 32);
+  const bool alloc = want && victim == XE_NONE;
+  unsigned int* next = alloc ? (unsigned int*)maps[m].hdr + 6 : (unsigned int*)K.err;  // hdr[3], low word
+  const uint32_t id = xe_wave_alloc_at(next, alloc);
+  if (want) en[0] = (en[0] & 0xffffffffull) | (uint64_t(alloc ? id : victim) << 32);
 }
 // ---- LRU evictions in a keyed batch (maps_hash_lru.go:114-119: an insert into a full map first deletes
 // UsageList[len-1]). In packet order the UsageList's tail is the least recently used value that no packet

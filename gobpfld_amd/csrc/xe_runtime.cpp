@@ -695,6 +695,17 @@ struct HostMap {
   bool links_stale = false;     // LRU: a parallel / keyed run left only stamps (lru_relink rebuilds the links)
   uint8_t* d_vsnap = nullptr; // LRU: the value pool at a parallel run's start (its adds are rolled back)
   uint64_t n_vsnap = 0;
+  // LRU: the device rollback point of a keyed or in-order run (lru_dev_snapshot): slot records, links,
+  // value lengths, values, stamps, header words — instead of downloading the map into the host mirror
+  // before every such run (48 MB over PCIe for a 1M-entry flow table)
+  uint64_t* d_rsnap = nullptr; uint64_t n_rsnap = 0;
+  uint32_t* d_lsnap = nullptr; uint64_t n_lsnap = 0;
+  uint32_t* d_esnap = nullptr; uint64_t n_esnap = 0;
+  uint8_t* d_vsnap2 = nullptr; uint64_t n_vsnap2 = 0;
+  uint64_t* d_tsnap2 = nullptr; uint64_t n_tsnap2 = 0;
+  uint64_t hsnap[8] = {0};
+  bool dsnap = false;         // the snapshot is the current run's start
+  bool snap_links_stale = false;
   bool ordered() const { return dkind == XE_DM_LRU || dkind == XE_DM_LIST || dkind == XE_DM_PERF; }
 
   uint64_t* key_at(uint32_t slot) { return keys.data() + uint64_t(slot) * kwords; }
@@ -1068,6 +1079,10 @@ void map_free_device(HostMap& m) {
   dev_free(m.d_tsnap);
   m.d_tsnap = nullptr;
   m.n_tsnap = 0;
+  dev_free(m.d_rsnap); dev_free(m.d_lsnap); dev_free(m.d_esnap); dev_free(m.d_vsnap2); dev_free(m.d_tsnap2);
+  m.d_rsnap = nullptr; m.d_lsnap = nullptr; m.d_esnap = nullptr; m.d_vsnap2 = nullptr; m.d_tsnap2 = nullptr;
+  m.n_rsnap = m.n_lsnap = m.n_esnap = m.n_vsnap2 = m.n_tsnap2 = 0;
+  m.dsnap = false;
   m.links_stale = false;
 }
 
@@ -1110,6 +1125,37 @@ int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s, bool renumber = false) {
       dsync(s))
     return -1;
   m.links_stale = false;
+  return 0;
+}
+
+template <class T>
+int ensure_dev(T** p, uint64_t& have, uint64_t need_elems);
+
+// An LRU map's device rollback point (see HostMap::d_rsnap): device-to-device copies of every array the
+// map lives in, taken at the start of a keyed or in-order run, so a rollback needs no host mirror
+int lru_dev_snapshot(HostMap& m, xe_stream_t s) {
+  const uint64_t rw = xe_hash_rwords(m.kwords), rec = uint64_t(m.cap + 1) * rw, pool = m.pool_cap;
+  const uint64_t vb = pool * m.def.value_size;
+  if (ensure_dev(&m.d_rsnap, m.n_rsnap, rec) || ensure_dev(&m.d_lsnap, m.n_lsnap, 4 * pool) ||
+      ensure_dev(&m.d_esnap, m.n_esnap, pool) || ensure_dev(&m.d_vsnap2, m.n_vsnap2, vb) ||
+      ensure_dev(&m.d_tsnap2, m.n_tsnap2, pool))
+    return -1;
+  if (d2d(m.d_rsnap, m.d_keys, rec * 8, s) || (pool && d2d(m.d_lsnap, m.d_link, 16 * pool, s)) ||
+      (pool && d2d(m.d_esnap, m.d_elen, 4 * pool, s)) || (vb && d2d(m.d_vsnap2, m.d_vals, vb, s)) ||
+      (pool && d2d(m.d_tsnap2, m.d_tag, 8 * pool, s)) || d2h(m.hsnap, m.d_hdr, 64, s) || dsync(s))
+    return -1;
+  m.dsnap = true;
+  m.snap_links_stale = m.links_stale;
+  return 0;
+}
+int lru_dev_restore(HostMap& m, xe_stream_t s) {
+  const uint64_t rw = xe_hash_rwords(m.kwords), rec = uint64_t(m.cap + 1) * rw, pool = m.pool_cap;
+  const uint64_t vb = pool * m.def.value_size;
+  if (d2d(m.d_keys, m.d_rsnap, rec * 8, s) || (pool && d2d(m.d_link, m.d_lsnap, 16 * pool, s)) ||
+      (pool && d2d(m.d_elen, m.d_esnap, 4 * pool, s)) || (vb && d2d(m.d_vals, m.d_vsnap2, vb, s)) ||
+      (pool && d2d(m.d_tag, m.d_tsnap2, 8 * pool, s)) || h2d(m.d_hdr, m.hsnap, 64, s) || dsync(s))
+    return -1;
+  m.links_stale = m.snap_links_stale;
   return 0;
 }
 
@@ -2369,6 +2415,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tm0).count(), n);
   };
   vm->staged_slot = -1;  // this run writes the maps outside the pipeline
+  for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dsnap = false;  // rollback points are per run
   if (stats) memset(stats, 0, sizeof *stats);
   if (int rc = xe_sync(vm)) return rc;  // pipelined batches first: they precede this one
   xe_stream_t s = stream ? (xe_stream_t)stream : vm->stream;
@@ -2459,8 +2506,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         if (d2d(m.d_keys, (uint8_t*)vm->d_ksnap + off, rb, s) || d2d(m.d_count, (uint8_t*)vm->d_ksnap + off + rb, 4, s)) return -1;
         off += rb + 8;
       }
-      for (size_t i = 1; i < vm->maps.size(); i++)  // the ordered maps come back from the host mirror
-        if (vm->maps[i].ordered() && ordered_upload(vm, vm->maps[i], vm->ord_slack, vm->ord_slack_bytes)) return -1;
+      for (size_t i = 1; i < vm->maps.size(); i++) {  // the ordered maps come back from their rollback point:
+        HostMap& m = vm->maps[i];                       // an LRU map's device snapshot, the others' host mirror
+        if (m.dkind == XE_DM_LRU && m.dsnap) {
+          if (lru_dev_restore(m, s)) return -1;
+        } else if (m.ordered() && ordered_upload(vm, m, vm->ord_slack, vm->ord_slack_bytes)) {
+          return -1;
+        }
+      }
     }
     if (keep_pkts && d2d(d_umem, vm->d_usnap, umem_len, s)) return -1;
     return dmemset(vm->d_aux, 0, aux_used * 8, s);
@@ -2489,8 +2542,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (int rc = snap_records()) return rc;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
-      if (m.ordered() && map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
-      if (m.dkind == XE_DM_LRU && lru_relink(vm, m, s)) return fail(vm, XE_ERR_DEVICE, "LRU relink");  // it promotes / evicts
+      if (m.dkind == XE_DM_LRU) {  // it promotes / evicts through the links; rollback point on the device
+        if (lru_relink(vm, m, s) || lru_dev_snapshot(m, s)) return fail(vm, XE_ERR_DEVICE, "LRU snapshot");
+      } else if (m.ordered() && map_download(vm, m)) {
+        return fail(vm, XE_ERR_DEVICE, "map download");
+      }
     }
     // the replay lane's packets are staged 64 at a time by the whole wave unless a packet may write
     // packet bytes a later packet reads (its window must then be fetched after the earlier writes)
@@ -2548,9 +2604,15 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     // rollbacks before any record was claimed
     std::vector<uint64_t> kh0;
     if (ordmaps) {
-      for (size_t i = 1; i < vm->maps.size(); i++)
-        if (vm->maps[i].ordered() && map_download(vm, vm->maps[i])) return fail(vm, XE_ERR_DEVICE, "map download");
-      tmark("map download");
+      for (size_t i = 1; i < vm->maps.size(); i++) {
+        HostMap& m = vm->maps[i];
+        if (m.dkind == XE_DM_LRU) {
+          if (lru_dev_snapshot(m, s)) return fail(vm, XE_ERR_DEVICE, "LRU snapshot");
+        } else if (m.ordered() && map_download(vm, m)) {
+          return fail(vm, XE_ERR_DEVICE, "map download");
+        }
+      }
+      tmark("map snapshot");
       if (ordered_hdr_read(vm, kh0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
       tmark("hdr read");
     }
@@ -2634,10 +2696,13 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         cnt = c32;
       } else {
         cnt = kh0[i * 8 + 2];
-        if (kh0[i * 8 + 3] + nd > m.pool_cap) {  // value ids for every new key: grow the pool, run again
-          if (krollback()) return -1;
+        // value ids for every new key that does not take over its victim's (keyed_lruid_item): grow the
+        // pool and run again
+        const uint64_t ev = cnt + nd > m.def.max_entries ? cnt + nd - m.def.max_entries : 0;
+        if (kh0[i * 8 + 3] + (nd - ev) > m.pool_cap) {
+          if (krollback() || map_download(vm, m)) return -1;  // the mirror: the batch's start
           vm->ord_slack = std::max<uint64_t>(vm->ord_slack, 2 * nd + 4096);
-          m.host_dirty = true;  // the mirror is the batch's start: rebuilt with the larger pool
+          m.host_dirty = true;  // rebuilt from the mirror with the larger pool
           if (prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "ordered map room");
           P.maps = vm->d_maps;
           keyed_trace("LRU pool grown");

@@ -44,6 +44,8 @@ WORKLOADS = {
                "map-entry writes, order-dependent; IMIX 64/576/1500 B",
     "c3lru": "C3-LRU: C3-learn over an LRU_HASH flow table (1M entries, 64K preloaded; every lookup hit and update "
              "promotes, misses insert; no eviction): keyed chains with the UsageList relinked by last touch",
+    "c3lrufull": "C3-LRU-full: C3-learn over a full LRU_HASH flow table (1M entries: 983,040 stale flows, then the 64K "
+                 "hot ones most recent); every learned flow evicts the least recently used entry",
     "c2rmw": "C2-RMW: C2 with the per-proto counter bumped by a plain load/add/store (value->packets++ without "
              "an atomic): the ordered read-modify-write, run in parallel through lift_rmw",
     "bpf2bpf": "bpf2bpf: call-heavy analogue of the reference's cmd/examples/bpf_to_bpf/src/xdp.c — Ethernet / IPv4 "
@@ -234,44 +236,57 @@ def ordered_paths(d_umem, d_desc, n: int, dev, stream, seq_sample: int = 65536) 
     return out
 
 
-def keyed_paths(dev, stream, n: int, reps: int = 3, seq_sample: int = 65536, name: str = "c3learn") -> dict:
-    """C3-learn (C3 with flow learning: a miss inserts the flow with bpf_map_update_elem; "c3lru": the same
-    over an LRU_HASH flow table) on fresh map state each run: the keyed ordered execution over all n
-    packets (SPEC pass, chains per written key, xe_internal.h) and, for scale, the one-lane in-order
-    replay (MODE_SEQUENTIAL) on the first `seq_sample` packets. Map upload and kernel compilation stay
-    outside the timed region (a 0-packet run first); the first run of each path is a warm-up."""
+def keyed_paths(dev, stream, n: int, batches: int = 5, seq_sample: int = 65536, name: str = "c3learn") -> dict:
+    """C3-learn (C3 with flow learning: a miss inserts the flow with bpf_map_update_elem), "c3lru" (the same
+    over an LRU_HASH flow table with room for every flow) or "c3lrufull" (the LRU table full: every learned
+    flow evicts the least recently used entry) as a steady stream: one VM, map upload and kernel builds
+    first (a 0-packet run, then one warm-up batch), then `batches` consecutive batches of n packets
+    (packets [k n, (k+1) n)) timed back to back, each on the keyed ordered execution path (SPEC pass,
+    chains per written key, xe_internal.h) as the VM's state carries over. For scale, the one-lane in-order
+    replay (MODE_SEQUENTIAL) of the first `seq_sample` packets on a fresh VM."""
     import torch
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import MODE_SEQUENTIAL, VM, Settings
-    umem, descs = W.build_batch(name, 0, n)
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
+    bufs = [device_batch(name, k * n, n, dev) for k in range(batches + 1)]
     d_ver = torch.zeros(n, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize(dev)
-    del umem
+    _dsync(dev)
     out = {"program": WORKLOADS[name]}
-    for key, mode, cnt, r in (("keyed", 0, n, reps), ("sequential_one_lane", MODE_SEQUENTIAL, seq_sample, 1)):
-        times, ks, modes, grids = [], [], set(), 0
-        for k in range(r + 1):
-            vm = VM(Settings(device=dev.index or 0, mode=mode))
-            W.setup_vm(vm, name)
-            vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), 0, stream=stream)  # upload
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            st = vm.run_batch_device(d_umem.data_ptr(), d_umem.numel(), d_desc.data_ptr(), cnt,
-                                     d_verdicts=d_ver.data_ptr(), stream=stream)
-            torch.cuda.synchronize(dev)
-            dt = time.perf_counter() - t0
-            if k:
-                times.append(dt)
-                ks.append(st["kernel_ms"])
-                modes.add(st["mode_used"])
-                grids = st["grid_blocks"]
-            vm.close()
-        dt = float(np.median(times))
-        out[key] = {"value": round(cnt / dt / 1e6, 3), "unit": "Mpkt/s", "packets": cnt, "ms_per_batch": round(dt * 1e3, 3),
-                    "device_ms": round(float(np.median(ks)), 3), "mode_used": sorted(modes), "grid_blocks": grids,
-                    "runs": len(times)}
+    vm = VM(Settings(device=dev.index or 0))
+    W.setup_vm(vm, name)
+    run = lambda b, cnt, v=vm: v.run_batch_device(b[0].data_ptr(), b[0].numel(), b[1].data_ptr(), cnt,
+                                                  d_verdicts=d_ver.data_ptr(), stream=stream)
+    run(bufs[0], 0)       # upload
+    run(bufs[0], n)       # warm-up batch (packets [0, n)): kernels, the keyed tables' sizes
+    _dsync(dev)
+    sts = []
+    t0 = time.perf_counter()
+    for k in range(1, batches + 1):
+        sts.append(run(bufs[k], n))
+    _dsync(dev)
+    dt = time.perf_counter() - t0
+    entries = vm.map_count(1) if hasattr(vm, "map_count") else None
+    vm.close()
+    out["keyed"] = {"value": round(batches * n / dt / 1e6, 3), "unit": "Mpkt/s", "packets_per_batch": n,
+                    "batches": batches, "ms_per_batch": round(dt / batches * 1e3, 3),
+                    "device_ms": [round(st["kernel_ms"], 3) for st in sts],
+                    "mode_used": [st["mode_used"] for st in sts], "grid_blocks": sts[-1]["grid_blocks"],
+                    "entries_after": entries,
+                    "what": f"a stream of {batches} consecutive batches on one VM after one warm-up batch (steady state)"}
+    # the one-lane replay, for scale
+    vm = VM(Settings(device=dev.index or 0, mode=MODE_SEQUENTIAL))
+    W.setup_vm(vm, name)
+    run(bufs[0], 0, vm)
+    _dsync(dev)
+    t0 = time.perf_counter()
+    st = run(bufs[0], seq_sample, vm)
+    _dsync(dev)
+    dt = time.perf_counter() - t0
+    vm.close()
+    out["sequential_one_lane"] = {"value": round(seq_sample / dt / 1e6, 3), "unit": "Mpkt/s", "packets": seq_sample,
+                                  "ms_per_batch": round(dt * 1e3, 3), "device_ms": round(st["kernel_ms"], 3),
+                                  "mode_used": [st["mode_used"]]}
+    del bufs
+    torch.cuda.empty_cache()
     return out
 
 
@@ -476,6 +491,22 @@ def device_batch(name: str, start: int, n: int, dev):
         descs = np.zeros(n, dtype=np_dtypes()[0])
         descs["addr"] = np.arange(n, dtype=np.int64) * size
         descs["len"] = size
+    elif cfg["pkt"] == "imix" and not cfg.get("frame"):
+        # mixed sizes, all >= 64 B: the header rows go to their packets' offsets on the device, 1M at a time
+        idx = np.arange(start, start + n, dtype=np.uint64)
+        sizes = W.packet_sizes(name, idx)
+        assert sizes.min() >= 64
+        offs, total = W.packet_offsets(name, sizes)
+        d_umem = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+        cols = torch.arange(64, dtype=torch.int64, device=dev)
+        for c0 in range(0, n, 1 << 20):
+            c1 = min(n, c0 + (1 << 20))
+            h = torch.from_numpy(W.headers(name, idx[c0:c1], 64)).to(dev)
+            pos = torch.from_numpy(offs[c0:c1]).to(dev)[:, None] + cols
+            d_umem[pos.reshape(-1)] = h.reshape(-1)
+        descs = np.zeros(n, dtype=np_dtypes()[0])
+        descs["addr"] = offs
+        descs["len"] = sizes
     else:
         umem, descs = W.build_batch(name, start, n)
         d_umem = torch.from_numpy(umem).to(dev)
@@ -638,6 +669,7 @@ def main() -> None:
         ordered = ordered_paths(d_umem, d_desc, n, dev, stream)
         ordered["keyed_c3learn"] = keyed_paths(dev, stream, args.keyed_packets)
         ordered["keyed_c3lru"] = keyed_paths(dev, stream, args.keyed_packets, name="c3lru")
+        ordered["keyed_c3lrufull"] = keyed_paths(dev, stream, args.keyed_packets, name="c3lrufull")
     # what the exchange ran over: the process group's backend and the rank count it saw (N > 1), and
     # RCCL's version; the C5 side line's per-flow delta exchange (time and bytes per GPU) beside it
     comm = {"backend": dist.get_backend() if world > 1 else None,

@@ -204,7 +204,11 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #endif
 #if !XE_GEN
 #undef XE_HAS_ORDERED
-#define XE_HAS_ORDERED 0  // LRU / queue / stack / perf maps and their helpers: general model only
+#if defined(XE_FIELDS_LRU) && XE_FIELDS_LRU
+#define XE_HAS_ORDERED 1  // the fields model over LRU_HASH maps (xe_jit.cpp lru_static: no queue / stack / perf)
+#else
+#define XE_HAS_ORDERED 0  // LRU / queue / stack / perf maps and their helpers: otherwise general model only
+#endif
 #elif !defined(XE_HAS_ORDERED)
 #define XE_HAS_ORDERED 1
 #endif
@@ -408,6 +412,8 @@ struct XeLane {
   uint32_t npres;         // PreservedRegisters depth = R10's frame index
   int32_t pi;             // program index (Registers.PI)
   uint32_t npristine;     // private ByteMemories still reading through to their source
+#endif
+#if XE_HAS_ORDERED
   uint32_t pidx;          // the packet's index in the batch (order key of its parallel appends)
   uint32_t oseq;          // appends the packet made so far
   uint32_t npops;         // list pops the packet made so far (parallel list operations, P.list)
@@ -1094,6 +1100,11 @@ XE_DEV int bm_prepare_write(XeLane& L, const XeParams& P, uint32_t h) {
   if (xe_h_cls(h) == XE_H_BMEM && *bm_field(L, xe_h_slot(h), XE_BM_MAT) == XE_NONE) return bm_materialize(L, P, xe_h_slot(h));
   return 0;
 }
+#endif
+
+#if !XE_GEN
+// the fields model has no private ByteMemories (clones exist only in the general model)
+XE_DEV int bm_before_write(XeLane&, const XeParams&, uint32_t) { return 0; }
 #endif
 
 // Go bounds check with wrapping add; passing the check with off >= len (overflow) panics at the index

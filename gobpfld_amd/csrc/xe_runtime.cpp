@@ -636,7 +636,9 @@ uint32_t next_pow2(uint64_t v) {
 // that no longer fits the 23-bit slot field of a value handle (xe_h_make), the largest table that does
 // (2^22 slots; probes run longer above half load, every entry still has a slot: MaxEntries <= cap).
 uint32_t hash_cap(uint32_t max_entries) {
-  uint32_t cap = next_pow2(uint64_t(max_entries) * 2);
+  uint64_t mult = 2;
+  if (const char* e = xe_tuning_env("XE_HASH_CAPX")) mult = uint64_t(std::max(2, atoi(e)));  // A/B: sparser tables
+  uint32_t cap = next_pow2(uint64_t(max_entries) * mult);
   const uint32_t lim = 1u << (XE_H_SLOT_BITS - 1);
   if (cap > lim && max_entries <= lim) cap = lim;
   return cap;

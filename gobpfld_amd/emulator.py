@@ -246,6 +246,12 @@ class VM:
         d = self.map_defs[m]
         self._check(self.lib.map_push(self.h, m, bytes(value).ljust(d.value_size, b"\0")), "map push")
 
+    def map_count(self, m: int) -> int:
+        """xe_map_count: the map's live entries (HASH / LRU_HASH), elements (QUEUE / STACK) or events."""
+        n = C.c_uint64(0)
+        self._check(self.lib.map_count(self.h, m, C.byref(n)), "map count")
+        return int(n.value)
+
     def map_values_bytes(self, m: int) -> int:
         b = C.c_uint64()
         self._check(self.lib.map_values_bytes(self.h, m, C.byref(b)), "map values bytes")

@@ -455,6 +455,35 @@ def headers_c3learn(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
     return _ipv4_l4_headers(3, idx, flow_tuples(3, fid), hdr)
 
 
+C3LRU_COLD_BASE = 1 << 21   # C3-LRU-full: flow ids of the stale entries that fill the table
+C3LRU_NEW_BASE = 1 << 22    # ... and of the flows its misses learn (disjoint from every preloaded one)
+
+
+def headers_c3lrufull(idx: np.ndarray, hdr: int = 64) -> np.ndarray:
+    """C3-learn's stream for the full LRU table: hits Zipf over the 64K hot flows, the 10% misses drawn
+    from C3_NEW_FLOWS flows that are in the table at no point before they are learned."""
+    r0 = rng_stream(3, idx, 0)
+    u = (r0 >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    hit = (rng_stream(3, idx, 2) % np.uint64(10)) != 0
+    fid = zipf_ranks(u, C3_FLOWS).astype(np.uint64)
+    new_id = np.uint64(C3LRU_NEW_BASE) + (rng_stream(3, idx, 3) % np.uint64(C3_NEW_FLOWS))
+    fid = np.where(hit, fid, new_id)
+    return _ipv4_l4_headers(3, idx, flow_tuples(3, fid), hdr)
+
+
+def c3lrufull_map_entries() -> tuple[np.ndarray, np.ndarray]:
+    """A full flow table (C3_MAX entries) in UsageList order of insertion: first the stale flows nobody
+    sends any more (C3_MAX - 64K of them), then the 64K hot flows from the coldest to the hottest, so the
+    hottest flow (rank 0) is the most recently used — the order steady traffic leaves an LRU table in."""
+    cold = np.uint64(C3LRU_COLD_BASE) + np.arange(C3_MAX - C3_FLOWS, dtype=np.uint64)
+    hot = np.arange(C3_FLOWS - 1, -1, -1, dtype=np.int64).astype(np.uint64)
+    fid = np.concatenate([cold, hot])
+    keys = key_from_tuple(flow_tuples(3, fid))
+    vals = np.zeros((len(fid), 16), dtype=np.uint8)
+    vals[:, 0:8] = (fid + np.uint64(1)).view(np.uint8).reshape(-1, 8)
+    return keys, vals
+
+
 def sizes_c3(idx: np.ndarray) -> np.ndarray:
     """IMIX-like {64: 7, 576: 4, 1500: 1}."""
     m = (rng_stream(3, idx, 5) % np.uint64(12)).astype(np.int64)
@@ -518,6 +547,7 @@ CONFIGS = {
     "c3": dict(program=prog_c3, pkt="imix", n=16 * 1024 * 1024),
     "c3learn": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
     "c3lru": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
+    "c3lrufull": dict(program=prog_c3learn, pkt="imix", n=16 * 1024 * 1024),
     "c4": dict(program=prog_c4, pkt=1500, n=16 * 1024 * 1024),
     # C4 in AF_XDP frames: 2-KiB chunks, the packet after the 256-byte XDP headroom (xsk.go:695-701
     # descriptors into a UMEM of fixed-size frames) instead of back to back
@@ -534,6 +564,8 @@ def workload_maps(name: str) -> list[tuple[MapDef, tuple[np.ndarray, np.ndarray]
         return [(MapDef(MAP_HASH, 16, 16, C3_MAX), c3_map_entries())]
     if name == "c3lru":  # the learning flow table as an LRU_HASH (room for every flow: no eviction)
         return [(MapDef(MAP_LRU_HASH, 16, 16, C3_MAX), c3_map_entries())]
+    if name == "c3lrufull":  # the LRU flow table full: every learned flow evicts the least recently used
+        return [(MapDef(MAP_LRU_HASH, 16, 16, C3_MAX), c3lrufull_map_entries())]
     if name == "c5":
         return [(MapDef(MAP_HASH, 16, 16, C5_MAX), c5_map_entries())]
     if name == "bpf2bpf":
@@ -550,7 +582,7 @@ def headers(name: str, idx: np.ndarray, hdr: int = 64) -> np.ndarray:
         for b in range(hdr):
             h[:, b] = (r >> np.uint64(8 * (b % 8))) & np.uint64(0xFF)
         return h
-    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c3lru": headers_c3learn, "c4": headers_c4, "c4f": headers_c4,
+    return {"c2": headers_c2, "c2rmw": headers_c2, "c3": headers_c3, "c3learn": headers_c3learn, "c3lru": headers_c3learn, "c3lrufull": headers_c3lrufull, "c4": headers_c4, "c4f": headers_c4,
             "c5": headers_c5, "bpf2bpf": headers_bpf2bpf}[name](idx, hdr)
 
 

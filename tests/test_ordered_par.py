@@ -246,15 +246,17 @@ def test_perf_appends_device_two_batches(gpu_lib, oracle_lib):
     assert len(gd) == len(od) and gd == od
 
 
-def _c3lru_run(lib, n, mode=None):
-    """C3-LRU (workloads: C3-learn over an LRU_HASH flow table) on one VM: results, verdicts, the table
-    and its UsageList."""
+def _c3lru_run(lib, n, mode=None, name="c3lru", batches=1):
+    """C3-LRU (workloads: C3-learn over an LRU_HASH flow table; "c3lrufull": the table full, so learning
+    evicts) on one VM over `batches` consecutive batches of n packets: the last batch's results and
+    statistics, the table and its UsageList."""
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
-    umem, descs = W.build_batch("c3lru", 0, n)
     vm = VM(Settings() if mode is None else Settings(mode=mode), lib=lib)
-    W.setup_vm(vm, "c3lru")
-    r = vm.run_batch(umem, descs)
+    W.setup_vm(vm, name)
+    for b in range(batches):
+        umem, descs = W.build_batch(name, b * n, n)
+        r = vm.run_batch(umem, descs)
     k, v = vm.map_dump(1)
     usage = vm.map_lru_order(1)
     vm.close()
@@ -289,6 +291,27 @@ def test_c3lru_device_keyed_equals_oracle(gpu_lib, oracle_lib):
     got = _c3lru_run(gpu_lib, n)
     assert got[0].stats["mode_used"] == MODE_KEYED, got[0].stats
     _same_c3lru(got, _c3lru_run(oracle_lib, n))
+
+
+@pytest.mark.gpu
+def test_c3lrufull_device_keyed_equals_oracle(gpu_lib, oracle_lib):
+    """C3-LRU-full: a full 1M-entry LRU flow table learning ~205K new flows from 4,194,304 IMIX packets, so
+    every learned flow evicts the least recently used entry (maps_hash_lru.go:114-119) — on the keyed path
+    with its evictions planned (xe_interp.h keyed_evict_item), against one sequential oracle VM: results,
+    verdicts, table and UsageList; then a second batch on the same VM (the steady state)."""
+    n = 4 * 1024 * 1024
+    got = _c3lru_run(gpu_lib, n, name="c3lrufull")
+    assert got[0].stats["mode_used"] == MODE_KEYED, got[0].stats
+    assert len(got[1]) == 1 << 20  # still full: every insert evicted one
+    _same_c3lru(got, _c3lru_run(oracle_lib, n, name="c3lrufull"))
+
+
+@pytest.mark.gpu
+def test_c3lrufull_two_batches_device(gpu_lib, oracle_lib):
+    n = 1 << 20
+    got = _c3lru_run(gpu_lib, n, name="c3lrufull", batches=2)
+    assert got[0].stats["mode_used"] == MODE_KEYED, got[0].stats
+    _same_c3lru(got, _c3lru_run(oracle_lib, n, name="c3lrufull", batches=2))
 
 
 def _lru_mixed_stream(lib, n=512):

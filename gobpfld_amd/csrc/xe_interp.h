@@ -413,7 +413,7 @@ struct XeLane {
   int32_t pi;             // program index (Registers.PI)
   uint32_t npristine;     // private ByteMemories still reading through to their source
 #endif
-#if XE_HAS_ORDERED
+#if XE_GEN || XE_HAS_ORDERED
   uint32_t pidx;          // the packet's index in the batch (order key of its parallel appends)
   uint32_t oseq;          // appends the packet made so far
   uint32_t npops;         // list pops the packet made so far (parallel list operations, P.list)
@@ -3034,6 +3034,9 @@ XE_DEV void lane_stage(XeLane& L, const XeParams& P, bool valid, uint64_t a, uin
   L.pi = P.entry;
   L.npops = 0;
   L.npristine = 0;
+#endif
+#if !XE_GEN && XE_HAS_ORDERED
+  L.npops = 0;
 #endif
   L.odef = 0x7eull;
   L.pkt = P.umem;

@@ -858,6 +858,20 @@ XE_DEV XeDevMap map_desc(const XeLane& L, uint32_t m) {
   return M;
 }
 
+// HASH / LRU_HASH value handles (xe_internal.h XE_H_BIG): slot (or value id) s of map m, and back
+XE_DEV uint32_t hv_make(const XeDevMap& M, uint32_t m, uint32_t s) {
+  if (s < (1u << XE_H_SLOT_BITS) || !M.big) return xe_h_make(XE_H_HASH, m, s);
+  return xe_h_make(XE_H_HASH, XE_H_BIG + 8u * (M.big - 1u) + (s >> XE_H_SLOT_BITS), s & ((1u << XE_H_SLOT_BITS) - 1u));
+}
+XE_DEV uint32_t hv_map(const XeParams& P, uint32_t h) {
+  const uint32_t m = xe_h_map(h);
+  return m >= XE_H_BIG ? uint32_t(P.bigmap[(m - XE_H_BIG) >> 3]) : m;
+}
+XE_DEV uint32_t hv_slot(uint32_t h) {
+  const uint32_t m = xe_h_map(h);
+  return (m >= XE_H_BIG ? ((m - XE_H_BIG) & 7u) << XE_H_SLOT_BITS : 0u) | xe_h_slot(h);
+}
+
 XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
   uint64_t vs = M.value_size;
   if (vs == 0) return ~0ull;
@@ -1010,7 +1024,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   }
 #endif
   uint32_t c = xe_h_cls(h);
-  uint32_t m = xe_h_map(h);
+  uint32_t m = c == XE_H_HASH ? hv_map(P, h) : xe_h_map(h);
   const XeDevMap M = map_desc(L, m);
   B.map = m;
   if (!XE_HAS_HASH || (XE_HAS_ARRAY && c == XE_H_ARRAY)) {
@@ -1030,13 +1044,13 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
     return true;
   }
   if (M.kind == XE_DM_LRU) {
-    const uint64_t vid = xe_h_slot(h);
+    const uint64_t vid = hv_slot(h);
     B.base = M.vals + vid * M.value_size;
     B.len = int64_t(((XE_GP(const uint32_t))M.elen)[vid]);
     return true;
   }
 #endif
-  uint32_t slot = xe_h_slot(h);
+  uint32_t slot = hv_slot(h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
   B.len = (uint32_t(((XE_GP(const uint64_t))M.keys)[uint64_t(slot) * M.rwords]) & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
   return true;
@@ -1052,12 +1066,12 @@ XE_DEV int key_touch_mem(XeLane& L, const XeParams& P, uint32_t h, const XeBMem&
   if (B.array) return key_touch_array(L, P, B.map, M, off, size, write, dkey);
   if (M.kind == XE_DM_LRU && xe_h_cls(h) == XE_H_HASH) {  // an LRU value: the key of its slot record
     if (h == L.kh) return key_touch(L, P, L.kk, write, dkey);
-    const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(xe_h_slot(h)) + 2];
+    const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(hv_slot(h)) + 2];
     return key_touch(L, P, kid_slot(B.map, M, slot), write, dkey);
   }
   // queue / stack elements and perf events follow packet order: a write to one is never keyed
   if (M.kind != XE_DM_HASH) return write ? XE_EV_ORD : 0;
-  return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, xe_h_slot(h)), write, dkey);
+  return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, hv_slot(h)), write, dkey);
 }
 #endif
 
@@ -1945,19 +1959,19 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
         // often as it was touched last; the run keeps each value's last touch (packet << 16 | call) + 1
         // and the runtime moves the touched keys to the UsageList's head by it (ordered_finalize)
         if (int e = lru_touch(L, M, v)) return e;
-        out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
+        out = XeReg{0, hv_make(M, m, v), XE_KIND_MEMPTR};
 #if XE_KEYED
         if (kid) { L.kh = out.h; L.kk = kid; }
 #endif
         return 0;
       }
       lru_promote(L, M, v);
-      out = XeReg{0, xe_h_make(XE_H_HASH, m, v), XE_KIND_MEMPTR};
+      out = XeReg{0, hv_make(M, m, v), XE_KIND_MEMPTR};
       return 0;
     }
 #endif
     int64_t slot = hash_find(M, kw, empty);
-    if (slot >= 0) out = XeReg{0, xe_h_make(XE_H_HASH, m, uint32_t(slot)), XE_KIND_MEMPTR};
+    if (slot >= 0) out = XeReg{0, hv_make(M, m, uint32_t(slot)), XE_KIND_MEMPTR};
 #if XE_KEYED
     if (slot >= 0 && kid) { L.kh = out.h; L.kk = kid; }
 #endif
@@ -2102,7 +2116,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
 #endif
     if (slot < 0) slot = hash_insert_new(M, kw, empty);
 #if XE_GEN
-    if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, uint32_t(slot)))) return e;
+    if (int e = bm_before_write(L, P, hv_make(M, m, uint32_t(slot)))) return e;
 #endif
     uint8_t* dst = M.vals + uint64_t(slot) * M.value_size;
     if (ve) {
@@ -2132,7 +2146,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       if (xe_concurrent(P)) return XE_EV_ORD;
       const uint32_t tail = uint32_t(*map_hdr(M, 1));
       if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
-      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, tail))) return e;
+      if (int e = bm_before_write(L, P, hv_make(M, m, tail))) return e;
       lru_erase(M, tail);  // evicted before the value is checked
     }
     if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
@@ -2184,10 +2198,10 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       if (int e = lru_insert(L, M, kw, empty, v)) return e;
     } else if (xe_concurrent(P)) {
       if (int e = lru_touch(L, M, v)) return e;  // appended + promoted, or promoted (:144-150)
-      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
+      if (int e = bm_before_write(L, P, hv_make(M, m, v))) return e;
     } else {
       lru_promote(L, M, v);
-      if (int e = bm_before_write(L, P, xe_h_make(XE_H_HASH, m, v))) return e;
+      if (int e = bm_before_write(L, P, hv_make(M, m, v))) return e;
     }
     uint8_t* dst = M.vals + uint64_t(v) * M.value_size;
     ((XE_GP(uint32_t))M.elen)[v] = ve ? 0u : M.value_size;
@@ -2654,7 +2668,7 @@ XE_DEV int uop_ldimm64(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm
 #endif
       int64_t slot = hash_find(M, kw, empty);
       if (slot < 0) return XE_E_MAP_NOT_PTR;
-      reg_replace(L, d, XE_KIND_MEMPTR, xe_h_make(XE_H_HASH, m, uint32_t(slot)), int64_t(u.x), 0);
+      reg_replace(L, d, XE_KIND_MEMPTR, hv_make(M, m, uint32_t(slot)), int64_t(u.x), 0);
       return 0;
     }
     return XE_EV_UNSUP;
@@ -2823,7 +2837,7 @@ XE_COLD int clone_mem(XeLane& L, const XeParams& P, uint32_t h, uint32_t& out) {
   if (c == XE_H_BMEM) info = *bm_field(L, xe_h_slot(h), XE_BM_INFO);
   else if (c == XE_H_PKT) info = XE_REGION_PACKET;
   else if (c == XE_H_ARRAY) info = XE_REGION_ARRAY | (xe_h_map(h) << 8);
-  else if (c == XE_H_HASH) info = XE_REGION_HASHVAL | (xe_h_map(h) << 8);
+  else if (c == XE_H_HASH) info = XE_REGION_HASHVAL | (hv_map(P, h) << 8);
   else info = (map_desc(L, xe_h_map(h)).kind == XE_DM_PERF ? XE_REGION_PERF : XE_REGION_QUEUEVAL) | (xe_h_map(h) << 8);
   *bm_field(L, uint32_t(k), XE_BM_SRC) = bm_ident(h);
   *bm_field(L, uint32_t(k), XE_BM_MAT) = XE_NONE;
@@ -3566,7 +3580,7 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
         g.kind[r] = uint8_t(k);
         if (k == XE_KIND_IMM || k == XE_KIND_NIL) { g.region[r] = 0xff; g.map[r] = 0; }
         else {
-          uint32_t c = xe_h_cls(R.h), rg = c, mp = (c == XE_H_ARRAY || c == XE_H_HASH) ? xe_h_map(R.h) : 0;
+          uint32_t c = xe_h_cls(R.h), rg = c, mp = c == XE_H_ARRAY ? xe_h_map(R.h) : c == XE_H_HASH ? hv_map(P, R.h) : 0;
 #if XE_GEN
           // clones report the region of the memory they copied (Clone keeps it, memory.go:109-116,212-219)
           if (c == XE_H_VCLONE) { rg = vc_src(L, xe_h_slot(R.h)); mp = 0; }

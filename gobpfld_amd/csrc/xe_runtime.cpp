@@ -639,7 +639,7 @@ uint32_t hash_cap(uint32_t max_entries) {
   uint64_t mult = 2;
   if (const char* e = xe_tuning_env("XE_HASH_CAPX")) mult = uint64_t(std::max(2, atoi(e)));  // A/B: sparser tables
   uint32_t cap = next_pow2(uint64_t(max_entries) * mult);
-  const uint32_t lim = 1u << (XE_H_SLOT_BITS - 1);
+  const uint32_t lim = 1u << (XE_H_SLOT_BITS + 2);  // slots of a big map's value handles (xe_internal.h XE_H_BIG)
   if (cap > lim && max_entries <= lim) cap = lim;
   return cap;
 }
@@ -651,6 +651,7 @@ struct HostMap {
   xe_map_def def{};
   uint32_t dkind = XE_DM_NONE;
   uint32_t cap = 0, kwords = 0;
+  uint32_t big = 0;  // HASH / LRU_HASH past the 23-bit handle slot field: 1 + its big-map number (XE_H_BIG)
   uint64_t vals_bytes = 0, vals_alloc = 0;
   std::vector<uint8_t> vals;
   std::vector<uint64_t> keys;
@@ -1444,6 +1445,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     d.key_size = m.def.key_size;
     d.value_size = m.def.value_size;
     d.max_entries = m.def.max_entries;
+    d.big = m.big;
     d.vals_bytes = m.vals_bytes;
     d.vals = m.d_vals;
     d.keys = m.d_keys;
@@ -1628,7 +1630,7 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_HASH;
       m.cap = hash_cap(def->max_entries);
-      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 4M)");
+      if (m.cap + 1 > (1u << (XE_H_SLOT_BITS + 3))) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 32M)");
       m.kwords = (def->key_size + 7) / 8;
       m.vals_bytes = uint64_t(m.cap + 1) * def->value_size;
       m.keys.assign(size_t(m.cap + 1) * m.kwords, 0);
@@ -1638,7 +1640,8 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_LRU;
       m.cap = hash_cap(def->max_entries);
-      if (m.cap + 1 >= (1u << XE_H_SLOT_BITS)) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 4M)");
+      if (m.cap + 1 > (1u << (XE_H_SLOT_BITS + 3)) || def->max_entries >= (1u << (XE_H_SLOT_BITS + 2)))
+        return fail(vm, XE_ERR_UNSUPPORTED, "LRU hash map max_entries too large (< 32M)");
       m.kwords = (def->key_size + 7) / 8;
       break;
     case XE_MAP_QUEUE: case XE_MAP_STACK:
@@ -1650,6 +1653,21 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
       break;
     default:  // AbstractMapToVM, emulator/maps.go:155
       return fail(vm, XE_ERR_MAPTYPE, "map type not yet implemented");
+  }
+  {
+    // value handles of slots / value ids past 23 bits (an LRU map's pool grows past MaxEntries) take the
+    // big-map encoding, which needs map indices below XE_H_BIG (xe_internal.h)
+    uint32_t nbig = 0;
+    for (size_t i = 1; i < vm->maps.size(); i++) nbig += vm->maps[i].big ? 1 : 0;
+    const bool big = (m.dkind == XE_DM_HASH && m.cap + 1 > (1u << XE_H_SLOT_BITS)) ||
+                     (m.dkind == XE_DM_LRU && (m.cap + 1 > (1u << XE_H_SLOT_BITS) || def->max_entries >= (1u << (XE_H_SLOT_BITS - 2))));
+    if (big) {
+      if (nbig >= XE_H_BIG_MAPS) return fail(vm, XE_ERR_UNSUPPORTED, "at most 4 hash maps above 4M entries");
+      if (vm->maps.size() > XE_H_BIG - 1) return fail(vm, XE_ERR_UNSUPPORTED, "a hash map above 4M entries must be among the first 31 maps");
+      m.big = nbig + 1;
+    } else if (nbig && vm->maps.size() > XE_H_BIG - 1) {
+      return fail(vm, XE_ERR_UNSUPPORTED, "at most 31 maps in a VM with a hash map above 4M entries");
+    }
   }
   m.vals_alloc = std::max<uint64_t>(8, (m.vals_bytes + 7) & ~uint64_t(7));
   m.vals.assign(m.vals_alloc, 0);
@@ -2228,6 +2246,8 @@ XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_
   P.desc = (const xe_desc*)d_desc;
   P.n = n;
   P.nmaps = uint32_t(vm->maps.size() - 1);
+  for (size_t i = 1; i < vm->maps.size(); i++)
+    if (vm->maps[i].big) P.bigmap[vm->maps[i].big - 1] = uint8_t(i);
   P.results = (xe_result*)d_results;
   P.verdicts = (uint32_t*)d_verdicts;
   P.regs = (xe_regs*)d_regs;

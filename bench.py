@@ -576,6 +576,8 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=0, help="oracle baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--engine", default="auto", choices=["auto", "interp", "jit"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "sequential"],
+                    help="sequential: every batch on the one-lane in-order path (profiling the replay)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     ap.add_argument("--no-ordered", action="store_true", help="skip the C2-RMW ordered-path lines (C2 only)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 side line (C2 only)")
@@ -625,7 +627,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)  # torch's stream vs the library's: the buffers are complete before any batch
 
     engine = {"auto": 0, "interp": 1, "jit": 2}[args.engine]
-    vm = VM(Settings(device=local, engine=engine))
+    from gobpfld_amd.emulator import MODE_AUTO, MODE_SEQUENTIAL
+    vm = VM(Settings(device=local, engine=engine, mode=MODE_SEQUENTIAL if args.mode == "sequential" else MODE_AUTO))
     W.setup_vm(vm, name)
     stream = torch.cuda.current_stream(dev).cuda_stream
     # A stream of batches through the pipelined entry point (each batch's conflict check runs on the

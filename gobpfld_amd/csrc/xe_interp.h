@@ -233,8 +233,21 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 
 // Paired deferral of 8-byte map adds (pend_add / pend_flush): the per-program kernel enables it when
 // a packet can make more than one such add; the interpreter keeps it on.
+// Committer wave (XE_COMMITTER, parallel mode, programs with paired adds): wave 3 of each block issues
+// the map-add atomics of waves 0..2, which hand their paired blocks over through an LDS ring. vmcnt counts
+// loads, stores and atomics together in issue order, so a wave that issues its own atomics waits for them
+// at its next header / probe wait (C5: the adds cost 0.63 of 2.04 ms, profiles/r5/c5_ab.json); the
+// committer never loads, so nothing waits on them but the committer itself.
+#if !defined(XE_COMMITTER) || !defined(__HIPCC__)
+#undef XE_COMMITTER
+#define XE_COMMITTER 0
+#endif
 #ifndef XE_PAIR_ADDS
 #define XE_PAIR_ADDS 1
+#endif
+#if XE_COMMITTER && !XE_PAIR_ADDS
+#undef XE_COMMITTER
+#define XE_COMMITTER 0
 #endif
 
 // Keyed ordered execution (XE_MODE_SPEC / XE_MODE_CHAIN, xe_internal.h): compiled into the interpreter
@@ -439,6 +452,9 @@ struct XeLane {
   uint32_t wave;            // global wave index (map value replica = wave % nrep)
   uint32_t awidth;          // atomic width classes used on maps 1..4 (4 bits per map)
   XePend* pend;             // this wave's deferred-atomic cache (LDS); null = apply immediately
+#if XE_COMMITTER
+  XE_LP(struct XeRing) ring;  // the committer's ring this wave's paired blocks go to (null: flush them itself)
+#endif
 #if XE_PAIR_ADDS
   // this packet's deferred 8-byte adds into one 16-byte block of a map value (pend_add): tag = block
   // address | map << 48 | word mask << 56, sums of word 0 / word 1; flushed by lane_finish, or by
@@ -1327,6 +1343,83 @@ XE_DEV void pend_flush(XeLane& L) {
   pend_word(L, L.pb_tag, L.pb_s1, 1);
 #endif
   L.pb_tag = L.pb_s0 = L.pb_s1 = 0;
+}
+#endif
+
+#if XE_COMMITTER
+// The committer's rings (LDS, one per producer wave): XE_RING_D chunks of paired blocks. A producer
+// writes a chunk's blocks and then its head; the committer applies a chunk (pend_flush's two wave atomics)
+// and then advances the tail. LDS operations of a wave complete in order and are visible to the block's
+// other waves once complete, so an lgkmcnt(0) wait between the data and the index write is the release.
+#define XE_RING_D 2
+struct XeRing {
+  unsigned int head, tail, done, pad;
+  unsigned long long tag[XE_RING_D][XE_WAVE], s0[XE_RING_D][XE_WAVE], s1[XE_RING_D][XE_WAVE];
+};
+XE_DEV void lds_release() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// (LDS address space throughout: a generic pointer would make these flat accesses, which count in vmcnt too)
+#define XE_RW(x) (*(XE_LP(volatile unsigned int))&(x))
+XE_DEV unsigned int ring_word(XE_LP(volatile unsigned int) w) {
+  const unsigned int v = *w;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return uint32_t(xe_readfirst(int(v)));
+}
+// producer (all lanes): this chunk's paired blocks to the committer instead of its own atomics
+XE_DEV void ring_put(XeLane& L, XE_LP(XeRing) R) {
+  const unsigned int h = ring_word(&XE_RW(R->head));  // only this wave writes head
+  uint32_t spins = 0;
+  while (h - ring_word(&XE_RW(R->tail)) >= XE_RING_D) {  // the committer has not taken chunk h - D yet
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins >= (1u << 26)) { pend_flush(L); return; }  // (unreachable: the committer runs until every producer is done)
+  }
+  const uint32_t s = h % XE_RING_D, lane = uint32_t(xe_lane());
+  R->tag[s][lane] = L.pb_tag;
+  R->s0[s][lane] = L.pb_s0;
+  R->s1[s][lane] = L.pb_s1;
+  lds_release();
+  if (lane == 0) XE_RW(R->head) = h + 1;
+  lds_release();
+  L.pb_tag = L.pb_s0 = L.pb_s1 = 0;
+}
+XE_DEV void ring_done(XE_LP(XeRing) R) {
+  lds_release();
+  if (xe_lane() == 0) XE_RW(R->done) = 1;
+  lds_release();
+}
+// the committer wave: apply every producer's chunks until all of them are done and drained. The bound
+// only guards against a protocol error (it sets XE_FLAG_CAPACITY: the batch replays, nothing is lost
+// silently); a producer finishes its walk in far fewer iterations.
+XE_DEV void committer_loop(XeLane& L, const XeParams& P, XE_LP(XeRing) rings, uint32_t nprod) {
+  const uint32_t lane = uint32_t(xe_lane()), w = lane & 1u;
+  unsigned int tail[4] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (uint32_t it = 0; it < (1u << 28); it++) {
+    bool progress = false, all = true;
+#pragma unroll
+    for (uint32_t p = 0; p < 3; p++) {
+      if (p >= nprod) break;
+      XE_LP(XeRing) R = rings + p;
+      const unsigned int done = ring_word(&XE_RW(R->done));  // done before head: a done producer's head is final
+      const unsigned int h = ring_word(&XE_RW(R->head));
+#pragma unroll 1
+      while (tail[p] != h) {
+        const uint32_t s = tail[p] % XE_RING_D;
+#pragma unroll
+        for (uint32_t hh = 0; hh < 2; hh++) {  // pend_flush: word w of lane j's block on lane 2j + w
+          const uint32_t src = 32u * hh + (lane >> 1);
+          pend_word(L, R->tag[s][src], w ? R->s1[s][src] : R->s0[s][src], w);
+        }
+        lds_release();  // the blocks are read before the slot is handed back
+        tail[p]++;
+        if (lane == 0) XE_RW(R->tail) = tail[p];
+        progress = true;
+      }
+      all = all && done && tail[p] == h;
+    }
+    if (all) return;
+    if (!progress) __builtin_amdgcn_s_sleep(1);
+  }
+  if (lane == 0) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
 }
 #endif
 
@@ -3614,7 +3707,10 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 
 // the stores lane_finish deferred (all lanes of the wave together)
 XE_DEV void lane_commit(XeLane& L, const XeParams& P) {
-#if XE_PAIR_ADDS
+#if XE_COMMITTER
+  if (L.ring) ring_put(L, L.ring);
+  else pend_flush(L);
+#elif XE_PAIR_ADDS
   pend_flush(L);
 #endif
   if (L.dv_i >= 0) P.verdicts[L.dv_i] = L.dv;
@@ -3646,6 +3742,9 @@ XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend*
   L.wave = wave;
   L.awidth = 0;
   L.pend = pend;
+#if XE_COMMITTER
+  L.ring = nullptr;
+#endif
   L.defer = false;
   L.dv_i = -1;
   L.dv = 0;

@@ -2587,7 +2587,19 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       vm->seq_scale *= 4;
       vm->ord_slack *= 4;
       vm->ord_slack_bytes *= 4;
-      if (rollback(true) || prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      if (rollback(true)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      // the ordered maps' room grows with the slack: an LRU map, back at its start state on the device,
+      // goes through the host mirror into a larger pool, and that becomes the next attempt's rollback point
+      for (size_t i = 1; i < vm->maps.size(); i++) {
+        HostMap& m = vm->maps[i];
+        if (m.dkind != XE_DM_LRU) continue;
+        m.dev_dirty = true;
+        if (map_download(vm, m)) return fail(vm, XE_ERR_DEVICE, "map download");
+        m.host_dirty = true;
+      }
+      if (prepare_run(vm, s)) return fail(vm, XE_ERR_DEVICE, "rollback");
+      for (size_t i = 1; i < vm->maps.size(); i++)
+        if (vm->maps[i].dkind == XE_DM_LRU && lru_dev_snapshot(vm->maps[i], s)) return fail(vm, XE_ERR_DEVICE, "LRU snapshot");
       P.maps = vm->d_maps;
     }
   };

@@ -121,3 +121,31 @@ def test_lru_evictions_device(gpu_lib, oracle_lib, case):
     make, modes = CASES[case]
     batches = make()
     _check(_run(gpu_lib, batches), _run(oracle_lib, batches), modes)
+
+
+def _grow_case(lib, max_entries=5000, n=7000):
+    """A full LRU map (max_entries live) and a batch of n inserts of new keys on the one-lane path: every
+    insert evicts, and the value pool runs out of room past the first few thousand inserts, so the replay
+    starts over from its rollback point with a larger pool."""
+    from gobpfld_amd.emulator import VM, MODE_SEQUENTIAL
+    vm = VM(Settings(mode=MODE_SEQUENTIAL), lib=lib)
+    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 4, max_entries))
+    keys = np.arange(max_entries, dtype=np.uint32)
+    vm.map_update_batch(m, keys.view(np.uint8).reshape(-1, 4), (keys + 1).view(np.uint8).reshape(-1, 4))
+    vm.set_entrypoint(vm.add_raw_program(_program()))
+    umem, descs = _batch(np.ones(n, dtype=np.uint32), 100000 + np.arange(n, dtype=np.uint32))
+    r = vm.run_batch(umem, descs)
+    out = (r.results.copy(), vm.map_lru_order(m), vm.map_count(m))
+    vm.close()
+    return out
+
+
+def test_lru_replay_pool_growth_hostsim(hostsim_lib, oracle_lib):
+    a, b = _grow_case(hostsim_lib), _grow_case(oracle_lib)
+    assert (a[0] == b[0]).all() and a[1] == b[1] and a[2] == b[2] == 5000
+
+
+@pytest.mark.gpu
+def test_lru_replay_pool_growth_device(gpu_lib, oracle_lib):
+    a, b = _grow_case(gpu_lib), _grow_case(oracle_lib)
+    assert (a[0] == b[0]).all() and a[1] == b[1] and a[2] == b[2] == 5000

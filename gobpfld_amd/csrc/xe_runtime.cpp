@@ -667,6 +667,7 @@ struct HostMap {
   std::array<uint8_t*, kAsyncDepth + 1> d_asnap{};
   uint8_t* d_rep = nullptr;  // nrep replicas of the value region (zero between runs)
   uint32_t nrep = 1;
+  bool nrep_fixed = false;  // nrep was chosen by a run (set_replicas)
   uint64_t rep_stride = 0;
   uint32_t lane = 0;    // width of the map adds of the last run (delta lanes): 0 none, 8 when mixed
   uint32_t wclass = 0;  // width classes of the last run's adds (bit 0: 1 B ... bit 3: 8 B)
@@ -1030,14 +1031,16 @@ int ensure_buf(void** p, size_t* cap, size_t need) {
 // HASH maps fold only their used slots (fold_map), so their bound is on the live bytes: C3's 64K hot
 // flows get 16 replicas (4 had a slow mode in 3 of 10 fresh processes: 2.13 ms against 1.0 ms,
 // profiles/r3/c3_modes.json); an ARRAY folds its whole region.
+// the fold reads the live bytes of every replica; the replicas themselves span the whole region (a
+// sparse HASH table's too), so their memory is bounded separately (C3: 16 x 32 MB)
+bool nrep_bounded(uint32_t want, uint64_t live, uint64_t vals_alloc, bool hash) {
+  return uint64_t(want) * (hash ? live : vals_alloc) <= (160ull << 20) && uint64_t(want) * vals_alloc <= (1ull << 30);
+}
+
 uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc, bool hash) {
   if (const char* e = xe_tuning_env("XE_NREP")) return uint32_t(std::min(16, std::max(1, atoi(e))));
   uint32_t want = live <= (2ull << 20) ? 16u : live <= (8ull << 20) ? 4u : 1u;
-  // the fold reads the live bytes of every replica; the replicas themselves span the whole region (a
-  // sparse HASH table's too), so their memory is bounded separately (C3: 16 x 32 MB)
-  while (want > 1 && (uint64_t(want) * (hash ? live : vals_alloc) > (160ull << 20) ||
-                      uint64_t(want) * vals_alloc > (1ull << 30)))
-    want >>= 1;
+  while (want > 1 && !nrep_bounded(want, live, vals_alloc, hash)) want >>= 1;
   return want;
 }
 
@@ -1053,6 +1056,7 @@ int map_alloc_device(HostMap& m) {
   if (dev_alloc((void**)&m.d_vals, m.vals_alloc)) return -1;
   if (dev_alloc((void**)&m.d_snap, m.vals_alloc)) return -1;
   m.nrep = 1;  // replicas are sized per run (set_replicas)
+  m.nrep_fixed = false;
   m.rep_stride = (m.vals_alloc + 255) & ~uint64_t(255);
   if (const char* e = xe_tuning_env("XE_REP_SKEW")) m.rep_stride = ((m.vals_alloc + 4095) & ~uint64_t(4095)) + uint64_t(atoll(e));
   if (m.dkind == XE_DM_HASH) {
@@ -1411,6 +1415,13 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
     }
     const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
     uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc, m.dkind == XE_DM_HASH) : 1u;
+    // the replica count is compiled into the per-program kernel: once chosen it stays while its fold stays
+    // bounded, so a table that grows over a stream of batches (C3-learn: 1 -> 5 MB live, 16 -> 4 replicas
+    // by the tiers) does not recompile mid-stream (a 9 s hiprtc compile in the measured stream)
+    if (m.nrep_fixed && want != m.nrep && !xe_tuning_env("XE_NREP") &&
+        (m.nrep == 1 || nrep_bounded(m.nrep, live, m.vals_alloc, m.dkind == XE_DM_HASH)))
+      want = m.nrep;
+    m.nrep_fixed = true;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)
       dev_free(m.d_rep);
       m.d_rep = nullptr;

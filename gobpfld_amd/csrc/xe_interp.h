@@ -1874,11 +1874,6 @@ XE_DEV int peek_key(const XeDevMap& M, uint64_t* kw, bool& empty) {
 // linked list over them (head = most recently used). link[4 v] = prev, [4 v + 1] = next, [4 v + 2] = slot.
 XE_DEV XE_GP(uint32_t) lru_link(const XeDevMap& M, uint32_t v, int f) { return (XE_GP(uint32_t))M.link + 4 * uint64_t(v) + f; }
 XE_DEV XE_GP(uint64_t) map_hdr(const XeDevMap& M, int w) { return (XE_GP(uint64_t))M.hdr + w; }
-XE_DEV void lru_unlink(const XeDevMap& M, uint32_t v) {
-  const uint32_t p = *lru_link(M, v, 0), n = *lru_link(M, v, 1);
-  if (p != XE_NONE) *lru_link(M, p, 1) = n; else *map_hdr(M, 0) = n;
-  if (n != XE_NONE) *lru_link(M, n, 0) = p; else *map_hdr(M, 1) = p;
-}
 // A value's stamp (M.tag[v]): its place in the UsageList as a number, larger = more recently used, 0 =
 // not in the list. Every touch writes the run's epoch (header word 5 = epoch << 48, set by the host per
 // run) plus a number that grows in packet order within the run, so the list is also "the live values by
@@ -1896,18 +1891,60 @@ XE_DEV uint64_t lru_stamp_seq(const XeDevMap& M) {  // one lane, packet order: t
   *map_hdr(M, 6) = c;
   return *map_hdr(M, 5) | (c & ((1ull << 48) - 1));
 }
-XE_DEV void lru_push_front(const XeDevMap& M, uint32_t v) {
-  const uint32_t h = uint32_t(*map_hdr(M, 0));
-  *lru_link(M, v, 0) = XE_NONE;
-  *lru_link(M, v, 1) = h;
-  if (h != XE_NONE) *lru_link(M, h, 0) = v; else *map_hdr(M, 1) = v;
-  *map_hdr(M, 0) = v;
+// The one-lane replay keeps no links either: its UsageList is an order log of touches in M.rec — word 0
+// the first entry that may be live, word 1 the end, then a ring of M.data_cap (a power of two) entries
+// {stamp, value id} from word 8. Every touch (promote, insert) appends; an entry is live while its stamp
+// is still its value's, so the first live entry is the least recently used value, the one an insert into
+// a full map evicts (maps_hash_lru.go:118-124, UsageList[len-1]). A touch is two stores instead of the
+// list's chain of dependent loads (unlink, push to the head). The runtime seeds the log with the live
+// values by stamp, oldest first, before each replay (xe_runtime.cpp lru_log_build), keeps data_cap at
+// least twice the pool (so a compaction always frees half of it) and after the replay rebuilds the links
+// from the stamps when something needs them, as after a parallel run (lru_relink).
+XE_DEV XE_GP(uint64_t) lru_log_at(const XeDevMap& M, uint64_t j) {
+  return (XE_GP(uint64_t))M.rec + 8 + 2 * (j & (M.data_cap - 1));
+}
+XE_DEV bool lru_log_live(const XeDevMap& M, uint64_t st, uint64_t v) { return ((XE_GP(const uint64_t))M.tag)[uint32_t(v)] == st; }
+XE_DEV void lru_log_compact(const XeDevMap& M) {  // the live entries moved up behind the first, in order
+  XE_GP(uint64_t) lg = (XE_GP(uint64_t))M.rec;
+  const uint64_t h = lg[0], t = lg[1];
+  uint64_t w = h;
+#pragma unroll 1
+  for (uint64_t r = h; r < t; r++) {
+    XE_GP(const uint64_t) e = lru_log_at(M, r);
+    const uint64_t st = e[0], v = e[1];
+    if (!lru_log_live(M, st, v)) continue;
+    XE_GP(uint64_t) o = lru_log_at(M, w++);
+    o[0] = st;
+    o[1] = v;
+  }
+  lg[1] = w;
+}
+XE_DEV void lru_log_push(const XeDevMap& M, uint32_t v, uint64_t st) {
+  XE_GP(uint64_t) lg = (XE_GP(uint64_t))M.rec;
+  if (lg[1] - lg[0] >= M.data_cap) lru_log_compact(M);
+  const uint64_t t = lg[1];
+  XE_GP(uint64_t) e = lru_log_at(M, t);
+  e[0] = st;
+  e[1] = v;
+  lg[1] = t + 1;
+}
+XE_DEV uint32_t lru_log_oldest(const XeDevMap& M) {  // the least recently used live value (XE_NONE: none)
+  XE_GP(uint64_t) lg = (XE_GP(uint64_t))M.rec;
+  uint64_t h = lg[0];
+  const uint64_t t = lg[1];
+  uint32_t v = XE_NONE;
+#pragma unroll 1
+  for (; h < t; h++) {
+    XE_GP(const uint64_t) e = lru_log_at(M, h);
+    if (lru_log_live(M, e[0], e[1])) { v = uint32_t(e[1]); break; }
+  }
+  lg[0] = h;
+  return v;
 }
 XE_DEV void lru_promote(XeLane& L, const XeDevMap& M, uint32_t v) {  // promote, :51-68
-  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp_seq(M);
-  if (uint32_t(*map_hdr(M, 0)) == v) return;
-  lru_unlink(M, v);
-  lru_push_front(M, v);
+  const uint64_t st = lru_stamp_seq(M);
+  ((XE_GP(uint64_t))M.tag)[v] = st;
+  lru_log_push(M, v, st);
 }
 XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_word0(M, uint64_t(slot)) >> 32); }
 // Concurrent modes: a touch (lookup hit, update) of value v by this packet — its last touch in packet order
@@ -1924,10 +1961,9 @@ XE_DEV uint32_t lru_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
 }
 // delete, :163-183 (evicted values keep their pool entry: pointers to them stay valid)
 XE_DEV void lru_erase(const XeDevMap& M, uint32_t v) {
-  ((XE_GP(uint64_t))M.tag)[v] = 0;  // out of the list
+  ((XE_GP(uint64_t))M.tag)[v] = 0;  // out of the list (its log entries are no longer live)
   const uint32_t slot = *lru_link(M, v, 2);
   ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_TOMB;
-  lru_unlink(M, v);
   *map_hdr(M, 2) -= 1;
 }
 XE_DEV int lru_insert(XeLane& L, const XeDevMap& M, const uint64_t* kw, bool empty, uint32_t& v) {
@@ -1940,8 +1976,9 @@ XE_DEV int lru_insert(XeLane& L, const XeDevMap& M, const uint64_t* kw, bool emp
   *lru_link(M, v, 2) = uint32_t(slot);
   ((XE_GP(uint32_t))M.elen)[v] = M.value_size;
   *map_hdr(M, 2) += 1;
-  ((XE_GP(uint64_t))M.tag)[v] = lru_stamp_seq(M);
-  lru_push_front(M, v);  // appended to the UsageList, then promoted to its top (:144-150)
+  const uint64_t st = lru_stamp_seq(M);  // appended to the UsageList, then promoted to its top (:144-150)
+  ((XE_GP(uint64_t))M.tag)[v] = st;
+  lru_log_push(M, v, st);
   return 0;
 }
 
@@ -2237,7 +2274,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     // insert, a chain's insert deletes the victim the build gave it (keyed_evict_item)
     if (v == XE_NONE && *map_hdr(M, 2) + 1 > M.max_entries && P.mode != XE_MODE_SPEC && P.mode != XE_MODE_CHAIN) {
       if (xe_concurrent(P)) return XE_EV_ORD;
-      const uint32_t tail = uint32_t(*map_hdr(M, 1));
+      const uint32_t tail = lru_log_oldest(M);
       if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
       if (int e = bm_before_write(L, P, hv_make(M, m, tail))) return e;
       lru_erase(M, tail);  // evicted before the value is checked

@@ -358,6 +358,27 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The one-lane replay's order log of an LRU map (xe_interp.h lru_log_push): the live values (the first
+// hdr[2] of `order`, the pool sorted by stamp, descending) oldest first as {stamp, value id}, from word 8
+__global__ void xe_lru_log_kernel(const uint64_t* tag, const uint32_t* order, const uint64_t* hdr, uint64_t* log) {
+  const uint64_t cnt = hdr[2];
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cnt; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t v = order[cnt - 1 - i];
+    log[8 + 2 * i] = tag[v];
+    log[9 + 2 * i] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    log[0] = 0;
+    log[1] = cnt;
+  }
+}
+extern "C" int xe_launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log,
+                                 hipStream_t s) {
+  const uint32_t blocks = pool / 256 + 1 < 8192 ? pool / 256 + 1 : 8192;
+  hipLaunchKernelGGL(xe_lru_log_kernel, dim3(blocks), dim3(256), 0, s, tag, order, hdr, log);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // keyed LRU evictions: the D table's LRU inserts sorted by (map, first inserting packet)
 extern "C" int xe_launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, hipStream_t s) {
   size_t tmp = 0;

@@ -49,6 +49,8 @@ extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* s
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                                     size_t* bytes, int renumber, hipStream_t s);
+extern "C" int xe_launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log,
+                                 hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
 extern "C" int xe_jit_occupancy(void* fn, uint32_t nmaps);
 extern "C" int xe_interp_occupancy(uint32_t nmaps);
@@ -265,6 +267,17 @@ int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link
   hdr[1] = cnt ? v[cnt - 1] : XE_NONE;
   return 0;
 }
+int launch_lru_log(const uint64_t* tag, uint32_t, const uint32_t* order, const uint64_t* hdr, uint64_t* log, xe_stream_t) {
+  const uint64_t cnt = hdr[2];  // xe_kernel.hip xe_lru_log_kernel: oldest first
+  for (uint64_t i = 0; i < cnt; i++) {
+    const uint32_t v = order[cnt - 1 - i];
+    log[8 + 2 * i] = tag[v];
+    log[9 + 2 * i] = v;
+  }
+  log[0] = 0;
+  log[1] = cnt;
+  return 0;
+}
 int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t) {
   if (!scratch) { *bytes = 8; return 0; }
   uint32_t acc = 0;
@@ -347,6 +360,9 @@ void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                       size_t* bytes, int renumber, xe_stream_t s) {
   return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, renumber, s);
+}
+int launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log, xe_stream_t s) {
+  return xe_launch_lru_log(tag, pool, order, hdr, log, s);
 }
 int launch_tail(const XeTailArgs* A, xe_stream_t s) { return xe_launch_tail(A, s); }
 int launch_desc_overlap(const void* desc, uint32_t n, uint64_t umem_len, void* scratch, size_t* bytes, uint32_t* flag,
@@ -1098,6 +1114,53 @@ void map_free_device(HostMap& m) {
 int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes);
 int ordered_download(xe_vm* vm, HostMap& m);
 
+// The device map table (XeDevMap per map) from the host maps; uploaded when it changed.
+int upload_map_table(xe_vm* vm, xe_stream_t s) {
+  std::vector<XeDevMap> dm(vm->maps.size());
+  memset(dm.data(), 0, dm.size() * sizeof(XeDevMap));
+  for (size_t i = 1; i < vm->maps.size(); i++) {
+    HostMap& m = vm->maps[i];
+    XeDevMap& d = dm[i];
+    d.kind = m.dkind;
+    d.btype = m.def.type;
+    d.key_size = m.def.key_size;
+    d.value_size = m.def.value_size;
+    d.max_entries = m.def.max_entries;
+    d.big = m.big;
+    d.vals_bytes = m.vals_bytes;
+    d.vals = m.d_vals;
+    d.keys = m.d_keys;
+    d.state = m.d_state;
+    d.count = m.d_count;
+    d.cap = m.cap;
+    d.kwords = m.kwords;
+    d.rwords = (m.dkind == XE_DM_HASH || m.dkind == XE_DM_LRU) ? xe_hash_rwords(m.kwords) : 0;
+    d.rep = m.d_rep;
+    d.rep_stride = m.rep_stride;
+    d.nrep = m.nrep;
+    d.hdr = m.d_hdr;
+    d.link = m.d_link;
+    d.elen = m.d_elen;
+    d.rec = m.d_rec;  // PERF: event records; LRU: the one-lane replay's order log (lru_log_build)
+    d.pool_cap = m.pool_cap;
+    d.list_cap = m.list_cap;
+    d.data_cap = m.data_cap;
+    d.tag = m.d_tag;
+  }
+  if (vm->d_maps_n < dm.size()) {
+    dev_free(vm->d_maps);
+    vm->d_maps = nullptr;
+    if (dev_alloc((void**)&vm->d_maps, dm.size() * sizeof(XeDevMap))) return fail(vm, XE_ERR_DEVICE, "device alloc (maps)");
+    vm->d_maps_n = dm.size();
+  }
+  if (vm->dm_uploaded.size() != dm.size() || memcmp(vm->dm_uploaded.data(), dm.data(), dm.size() * sizeof(XeDevMap))) {
+    if (h2d(vm->d_maps, dm.data(), dm.size() * sizeof(XeDevMap), s) || dsync(s))
+      return fail(vm, XE_ERR_DEVICE, "map table upload");
+    vm->dm_uploaded = dm;
+  }
+  return XE_OK;
+}
+
 int map_upload(xe_vm* vm, HostMap& m) {
   if (m.ordered()) return ordered_upload(vm, m, vm->ord_slack, vm->ord_slack_bytes);
   if (h2d(m.d_vals, m.vals.data(), m.vals_alloc, vm->stream)) return -1;
@@ -1137,6 +1200,28 @@ int lru_relink(xe_vm* vm, HostMap& m, xe_stream_t s, bool renumber = false) {
 
 template <class T>
 int ensure_dev(T** p, uint64_t& have, uint64_t need_elems);
+
+// The one-lane replay's order log of an LRU map (xe_interp.h lru_log_push, in d_rec): room for twice the
+// pool, seeded with the live values by stamp, oldest first (the stamps sorted on the device, as lru_relink
+// does). 1: the log was (re)allocated and the map table must be uploaded again; 0; -1 on error.
+const uint32_t* lru_sorted_ids(const void* scratch, uint32_t pool);
+int lru_log_build(xe_vm* vm, HostMap& m, xe_stream_t s) {
+  uint64_t cap = 1024;
+  while (cap < 2ull * m.pool_cap) cap <<= 1;
+  int grown = 0;
+  if (m.data_cap < cap) {
+    if (ensure_dev(&m.d_rec, m.n_rec, 8 + 2 * cap)) return -1;
+    m.data_cap = cap;
+    grown = 1;
+  }
+  size_t bytes = 0;
+  if (launch_lru_relink(m.d_tag, m.pool_cap, m.pool_cap, m.d_link, m.d_hdr, nullptr, &bytes, 2, s) ||
+      ensure_buf(&vm->d_relink, &vm->d_relink_cap, bytes) ||
+      launch_lru_relink(m.d_tag, m.pool_cap, m.pool_cap, m.d_link, m.d_hdr, vm->d_relink, &bytes, 2, s) ||
+      launch_lru_log(m.d_tag, m.pool_cap, lru_sorted_ids(vm->d_relink, m.pool_cap), m.d_hdr, m.d_rec, s))
+    return -1;
+  return grown;
+}
 
 // An LRU map's device rollback point (see HostMap::d_rsnap): device-to-device copies of every array the
 // map lives in, taken at the start of a keyed or in-order run, so a rollback needs no host mirror
@@ -1446,48 +1531,7 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       fprintf(stderr, "{\"map\": %zu, \"vals\": \"%p\", \"keys\": \"%p\", \"rep\": \"%p\", \"nrep\": %u, \"rep_stride\": %llu}\n",
               i, (void*)m.d_vals, (void*)m.d_keys, (void*)m.d_rep, m.nrep, (unsigned long long)m.rep_stride);
   }
-  std::vector<XeDevMap> dm(vm->maps.size());
-  memset(dm.data(), 0, dm.size() * sizeof(XeDevMap));
-  for (size_t i = 1; i < vm->maps.size(); i++) {
-    HostMap& m = vm->maps[i];
-    XeDevMap& d = dm[i];
-    d.kind = m.dkind;
-    d.btype = m.def.type;
-    d.key_size = m.def.key_size;
-    d.value_size = m.def.value_size;
-    d.max_entries = m.def.max_entries;
-    d.big = m.big;
-    d.vals_bytes = m.vals_bytes;
-    d.vals = m.d_vals;
-    d.keys = m.d_keys;
-    d.state = m.d_state;
-    d.count = m.d_count;
-    d.cap = m.cap;
-    d.kwords = m.kwords;
-    d.rwords = (m.dkind == XE_DM_HASH || m.dkind == XE_DM_LRU) ? xe_hash_rwords(m.kwords) : 0;
-    d.rep = m.d_rep;
-    d.rep_stride = m.rep_stride;
-    d.nrep = m.nrep;
-    d.hdr = m.d_hdr;
-    d.link = m.d_link;
-    d.elen = m.d_elen;
-    d.rec = m.d_rec;
-    d.pool_cap = m.pool_cap;
-    d.list_cap = m.list_cap;
-    d.data_cap = m.data_cap;
-    d.tag = m.d_tag;
-  }
-  if (vm->d_maps_n < dm.size()) {
-    dev_free(vm->d_maps);
-    vm->d_maps = nullptr;
-    if (dev_alloc((void**)&vm->d_maps, dm.size() * sizeof(XeDevMap))) return fail(vm, XE_ERR_DEVICE, "device alloc (maps)");
-    vm->d_maps_n = dm.size();
-  }
-  if (vm->dm_uploaded.size() != dm.size() || memcmp(vm->dm_uploaded.data(), dm.data(), dm.size() * sizeof(XeDevMap))) {
-    if (h2d(vm->d_maps, dm.data(), dm.size() * sizeof(XeDevMap), s) || dsync(s))
-      return fail(vm, XE_ERR_DEVICE, "map table upload");
-    vm->dm_uploaded = dm;
-  }
+  if (int rc = upload_map_table(vm, s)) return rc;
   if (!vm->d_aux && dev_alloc((void**)&vm->d_aux, kAuxWords * 8)) return fail(vm, XE_ERR_DEVICE, "device alloc (aux)");
   return XE_OK;
 }
@@ -2575,8 +2619,8 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     if (int rc = snap_records()) return rc;
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
-      if (m.dkind == XE_DM_LRU) {  // it promotes / evicts through the links; rollback point on the device
-        if (lru_relink(vm, m, s) || lru_dev_snapshot(m, s)) return fail(vm, XE_ERR_DEVICE, "LRU snapshot");
+      if (m.dkind == XE_DM_LRU) {  // rollback point on the device (the replay keeps its own order log)
+        if (lru_dev_snapshot(m, s)) return fail(vm, XE_ERR_DEVICE, "LRU snapshot");
       } else if (m.ordered() && map_download(vm, m)) {
         return fail(vm, XE_ERR_DEVICE, "map download");
       }
@@ -2587,13 +2631,28 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (int attempt = 0;; attempt++) {
       P.mode = XE_MODE_SEQUENTIAL;
       if (general && ensure_arena(vm, true, 1, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (replay arena)");
+      bool table = false;  // the LRU maps' order logs from their stamps (the run's start state)
+      for (size_t i = 1; i < vm->maps.size(); i++) {
+        if (vm->maps[i].dkind != XE_DM_LRU) continue;
+        const int r = lru_log_build(vm, vm->maps[i], s);
+        if (r < 0) return fail(vm, XE_ERR_DEVICE, "LRU order log");
+        table = table || r > 0;
+      }
+      if (table) {
+        if (int rc = upload_map_table(vm, s)) return rc;
+        P.maps = vm->d_maps;
+      }
       vm->t1.rec(s);
       if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t2.rec(s);
       if (hostcalls && serve_hostcalls(vm->h_hostcall, s)) return fail(vm, XE_ERR_DEVICE, "kernel failed (host helpers)");
       if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
       ms += Timer::ms(vm->t1, vm->t2);
-      if (!(red[0] & XE_FLAG_CAPACITY)) return XE_OK;
+      if (!(red[0] & XE_FLAG_CAPACITY)) {
+        for (size_t i = 1; i < vm->maps.size(); i++)  // the replay kept stamps and its log, not the links
+          if (vm->maps[i].dkind == XE_DM_LRU) vm->maps[i].links_stale = true;
+        return XE_OK;
+      }
       if (attempt >= 6) return fail(vm, XE_ERR_NOMEM, "the ordered replay outgrew its device arena");
       vm->seq_scale *= 4;
       vm->ord_slack *= 4;

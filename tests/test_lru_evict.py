@@ -149,3 +149,36 @@ def test_lru_replay_pool_growth_hostsim(hostsim_lib, oracle_lib):
 def test_lru_replay_pool_growth_device(gpu_lib, oracle_lib):
     a, b = _grow_case(gpu_lib), _grow_case(oracle_lib)
     assert (a[0] == b[0]).all() and a[1] == b[1] and a[2] == b[2] == 5000
+
+
+def _churn_case(lib, batches=3, n=40000):
+    """The one-lane replay's order log (xe_interp.h lru_log_push), in packet order: a small LRU map under
+    lookups and updates — touches that outnumber the log's room (16,384 entries for this map) with no
+    eviction to clear it (compactions), then evictions that skip the dead entries of values touched again
+    since; the log seeded again from the stamps for each batch."""
+    from gobpfld_amd.emulator import VM
+    vm = VM(Settings(mode=MODE_SEQUENTIAL), lib=lib)
+    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 4, MAX))
+    vm.set_entrypoint(vm.add_raw_program(_program()))
+    rng = np.random.default_rng(77)
+    out = []
+    for b in range(batches):
+        ops = (rng.random(n) < 0.08).astype(np.uint32)  # few inserts: the pool keeps its first size
+        # the first 3/4 of each batch over half the map's room in keys (no evictions: the log fills up
+        # and compacts), the rest over four times its room (evictions skip the log's dead entries)
+        keys = rng.zipf(1.3, size=n).astype(np.uint32) % (MAX // 2)
+        keys[3 * n // 4:] = rng.integers(0, 4 * MAX, size=n - 3 * n // 4)
+        r = vm.run_batch(*_batch(ops, keys))
+        k, v = vm.map_dump(m)
+        out.append((r.results.copy(), r.stats["mode_used"], vm.map_lru_order(m), bytes(np.asarray(k)), bytes(np.asarray(v))))
+    vm.close()
+    return out
+
+
+def test_lru_order_log_churn_hostsim(hostsim_lib, oracle_lib):
+    _check(_churn_case(hostsim_lib), _churn_case(oracle_lib), [MODE_SEQUENTIAL] * 3)
+
+
+@pytest.mark.gpu
+def test_lru_order_log_churn_device(gpu_lib, oracle_lib):
+    _check(_churn_case(gpu_lib), _churn_case(oracle_lib), [MODE_SEQUENTIAL] * 3)

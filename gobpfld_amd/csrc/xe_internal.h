@@ -398,7 +398,7 @@ struct XeParams {
   const uint32_t* poison;
   // sequential mode: stage the next 64 packets' descriptors and header windows with the whole wave
   // (no program of the VM writes packet bytes), then run them one after another on lane 0
-  uint32_t seq_prefetch;
+  uint32_t seq_prefetch;  // sequential mode: 1 = the wave stages 64 packets at a time, 2 = and runs ahead (XE_SEQ_PEEK)
   // keyed ordered execution (XE_MODE_SPEC / XE_MODE_CHAIN, and the skip mask of its parallel pass)
   XeKeyed K;
   // chunk -> wave schedule of the parallel pass (xe_debug_set_schedule): 0 = wave w walks chunks

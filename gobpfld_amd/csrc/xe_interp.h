@@ -318,6 +318,9 @@ XE_DEV void xe_wave_count(unsigned int* p, bool want) {
 #define XE_EV_ORD 0x4000
 #define XE_EV_EXIT 0x8000
 #define XE_EV_STOP 0x6000  // the count pass of parallel list operations: the lane's packet stops here
+#ifndef XE_SEQ_PEEK
+#define XE_SEQ_PEEK 0  // the one-lane replay's runahead (seq_packets), per-program kernels only
+#endif
 #define XE_EV_CLASS(e) ((e) & 0xf000)
 #define XE_IS_PANIC(e) (XE_EV_CLASS(e) == XE_EV_PANIC)
 
@@ -432,6 +435,9 @@ struct XeLane {
   uint32_t npops;         // list pops the packet made so far (parallel list operations, P.list)
 #endif
   uint64_t odef;      // ids 1..6 still holding their ctx default
+#if XE_SEQ_PEEK
+  int peek;           // the runahead of the one-lane replay is running (seq_packets; wave-uniform)
+#endif
   // packet
   uint8_t* pkt;
   int64_t plen;
@@ -1020,6 +1026,16 @@ struct XeBMem {
 
 // Map memories — and, in the general model, list / perf elements and lane-private ByteMemories (a
 // clone still reading through resolves to its source). The packet itself takes the header-window path.
+// the lane runs the one-lane replay's runahead (seq_packets): shared writes stop its packet there
+XE_DEV bool xe_peeking(const XeLane& L) {
+#if XE_SEQ_PEEK
+  return xe_readfirst(L.peek) != 0;
+#else
+  (void)L;
+  return false;
+#endif
+}
+
 XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem& B) {
 #if XE_GEN
   while (xe_h_cls(h) == XE_H_BMEM) {
@@ -2095,7 +2111,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
 #endif
         return 0;
       }
-      lru_promote(L, M, v);
+      if (!xe_peeking(L)) lru_promote(L, M, v);
       out = XeReg{0, hv_make(M, m, v), XE_KIND_MEMPTR};
       return 0;
     }
@@ -2109,6 +2125,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
   }
 #if XE_HAS_ORDERED
   if (M.kind == XE_DM_LIST || M.kind == XE_DM_PERF) {
+    if (xe_peeking(L)) return XE_EV_STOP;
     // the list changes in packet order: in parallel only through the list-run rules (list_par)
     if (xe_concurrent(P) && !(M.kind == XE_DM_LIST && list_par(P))) return XE_EV_ORD;
     // count pass: the packet's rank needs only its pops before here (none): it stops (a later pop of it
@@ -2485,6 +2502,7 @@ XE_COLD int host_helper(XeLane& L, const XeParams& P, uint32_t id) {
 
 XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = XE_CM_ALL, uint32_t cm2 = XE_CM_ALL,
                        uint32_t cm3 = XE_CM_ALL) {
+  if (xe_peeking(L) && fn != 1) return XE_EV_STOP;
   if (fn >= 192) return XE_E_NO_HELPER;
   if (fn < 0) return XE_EV_PANIC | XE_P_INDEX;
 #if XE_HELPER_TABLE
@@ -2827,6 +2845,7 @@ XE_DEV int uop_store(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd 
   const XeReg D = reg_get(L, u.dst);
   XE_NILCHK(D);
   if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  if (xe_peeking(L) && !is_vm_cls(xe_h_cls(D.h))) return XE_EV_STOP;
   const int64_t off = ptr_eff(D, u.tgt);
   const int size = uop_size(u);
   if ((cmd & XE_CM_MAPS) && (u.fl & UF_LIFT) && lift_active(P)) {
@@ -2864,6 +2883,7 @@ XE_DEV int uop_atomic(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cmd
   const XeReg D = reg_get(L, u.dst);
   XE_NILCHK(D);
   if ((cmd & XE_CM_IMM) && XE_T_KIND(D.t) == XE_KIND_IMM) return XE_E_NONPTR_STORE;
+  if (xe_peeking(L) && !is_vm_cls(xe_h_cls(D.h))) return XE_EV_STOP;
   const uint32_t h = D.h;
   const int64_t off = ptr_eff(D, u.tgt);
   const int size = uop_size(u);
@@ -2937,6 +2957,7 @@ XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1
 // in a per-program kernel: a VM with a host or nil helper runs on the interpreter).
 XE_DEV int uop_helper_key(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1, uint32_t cm2, uint32_t cm3,
                           const uint64_t* kp) {
+  if (xe_peeking(L) && u.imm != 1) return XE_EV_STOP;
   return u.imm == 1 ? helper_lookup(L, P, cm1, cm2, kp) : helper_update(L, P, cm1, cm2, cm3, kp);
 }
 
@@ -3223,8 +3244,14 @@ XE_DEV void lane_commit(XeLane& L, const XeParams& P);
 // chain is the program's own work instead of descriptor -> window -> program round trips; without it
 // (a program may write packet bytes a later packet reads) each packet is fetched just before it runs.
 // body(i, valid) runs the staged packet on the lanes where valid and calls lane_finish (all lanes).
-template <class Body>
-XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
+//
+// Runahead (P.seq_prefetch & 2, per-program kernels with XE_SEQ_PEEK): before the replay lane runs the
+// 64 staged packets, every lane runs its own one with all shared writes stopped (xe_peeking: a store or
+// atomic outside the lane's stack, any helper but bpf_map_lookup_elem, an LRU lookup's promotion), and
+// its results dropped. What it leaves behind is the map lines its lookups read — hash probes, values —
+// in this CU's caches, so the replay lane's dependent loads hit there instead of going to HBM one at a time.
+template <class Body, class Peek>
+XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body, Peek peek) {
   const uint32_t lane = uint32_t(xe_lane());
   for (uint32_t c0 = 0; c0 < P.n; c0 += XE_WAVE) {
     const uint32_t m = P.n - c0 < XE_WAVE ? P.n - c0 : XE_WAVE;
@@ -3236,6 +3263,14 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body) {
       desc_fetch(P, c0 + lane, v, a, l);
       f = hdr_issue(P, L.hdrbuf, a, l, v);
       hdr_wait();
+#if XE_SEQ_PEEK
+      if (P.seq_prefetch & 2u) {
+        lane_stage(L, P, v, a, l, f, L.hdrbuf, int(lane));
+        L.peek = 1;
+        peek(v);
+        L.peek = 0;
+      }
+#endif
     }
 #pragma unroll 1
     for (uint32_t k = 0; k < m; k++) {
@@ -3771,6 +3806,9 @@ XE_DEV void stage_maps(XeLane& L, const XeParams& P, XE_LP(XeDevMap) lds) {
 }
 
 XE_DEV void wave_state_init(XeLane& L, const XeParams& P, uint32_t wave, XePend* pend) {
+#if XE_SEQ_PEEK
+  L.peek = 0;
+#endif
 #if XE_GEN
   L.G = &P.gen;
   L.gl = P.mode == XE_MODE_SEQUENTIAL ? 0u : wave * XE_WAVE + uint32_t(xe_lane());
@@ -3839,7 +3877,8 @@ XE_COLD void trace_put(XeLane& L, const XeParams& P, int32_t slot, uint32_t i, u
 }
 #endif
 
-XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
+// finish = false: the runahead of the one-lane replay (seq_packets), no records, no trace
+XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid, bool finish = true) {
   int status = valid ? -1 : XE_ST_OK;  // -1 = running
   int code = 0;
   int32_t pc = 0, res_pc = 0;
@@ -3849,7 +3888,7 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
   L.oseq = 0;
 #endif
 #if XE_TRACE
-  const int32_t tslot = valid && P.trace ? trace_slot(P, i) : -1;
+  const int32_t tslot = finish && valid && P.trace ? trace_slot(P, i) : -1;
   uint64_t tdone = 0;  // steps that completed
 #endif
 
@@ -3895,7 +3934,7 @@ XE_DEV void run_staged(XeLane& L, const XeParams& P, uint32_t i, bool valid) {
 #if XE_TRACE
   if (tslot >= 0) P.trace_cnt[tslot] = uint32_t(tdone < P.trace_max ? tdone : P.trace_max);
 #endif
-  lane_finish(L, P, i, valid, status, code, res_pc, steps);
+  if (finish) lane_finish(L, P, i, valid, status, code, res_pc, steps);
 }
 
 XE_DEV void run_packet(XeLane& L, const XeParams& P, uint32_t i, bool valid) {

@@ -21,7 +21,7 @@ extern "C" __global__ void __launch_bounds__(256) xe_interp_kernel(XeParams P) {
   wave_state_init(L, P, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, &pend_lds[threadIdx.x >> 6]);
   if (P.mode == XE_MODE_SEQUENTIAL) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
-    seq_packets(L, P, [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });
+    seq_packets(L, P, [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); }, [](bool) {});
   } else if (P.mode == XE_MODE_CHAIN) {
     chain_packets(L, P, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
                   [&](uint32_t i, bool valid) { run_staged(L, P, i, valid); });

@@ -22,6 +22,9 @@
 #include <vector>
 
 #ifdef XE_HOSTSIM
+// the host simulation runs the one-lane replay's runahead too (seq_packets): every packet runs once with
+// its shared writes stopped before it runs for real, so the CPU tests see any effect that leaks from it
+#define XE_SEQ_PEEK 1
 #include "xe_interp.h"
 typedef void* xe_stream_t;
 #else
@@ -98,7 +101,8 @@ int launch_interp(const XeParams* P, uint32_t, uint32_t, xe_stream_t) {
   } else if (P->mode == XE_MODE_CHAIN) {
     chain_packets(L, *P, 0, 1, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
   } else {
-    seq_packets(L, *P, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); });
+    seq_packets(L, *P, [&](uint32_t i, bool valid) { run_staged(L, *P, i, valid); },
+                [&](bool valid) { run_staged(L, *P, 0, valid, false); });
   }
   flush_wave_state(L, *P);
   return 0;
@@ -2628,6 +2632,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     // the replay lane's packets are staged 64 at a time by the whole wave unless a packet may write
     // packet bytes a later packet reads (its window must then be fetched after the earlier writes)
     P.seq_prefetch = may_write_packet(vm->programs[vm->entry]) ? 0u : 1u;
+    // and run ahead of the lane (per-program kernels; XE_SEQ_PEEK=0 in the tuning build: A/B)
+    if (P.seq_prefetch) {
+      const char* pk = xe_tuning_env("XE_SEQ_PEEK");
+      if (!pk || atoi(pk)) P.seq_prefetch |= 2u;
+    }
     for (int attempt = 0;; attempt++) {
       P.mode = XE_MODE_SEQUENTIAL;
       if (general && ensure_arena(vm, true, 1, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (replay arena)");

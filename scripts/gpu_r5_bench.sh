@@ -26,4 +26,4 @@ else
   done
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_bpf2bpf -o run --output-format csv -- python3 bench.py --config bpf2bpf --steps 10 --warmup 2 $B > $OUT/prof_bpf2bpf.log 2>&1 || { echo "prof bpf2bpf failed"; tail -3 $OUT/prof_bpf2bpf.log; exit 1; }
 fi
-echo "all done"
+find $OUT -name "*.db" -delete; du -sh $OUT; echo "all done"

@@ -11,9 +11,9 @@ for c in ${CONFIGS:-c2rmw c3learn c3lru c3lrufull}; do
   timeout -k 10 240 python bench.py $B > $OUT/$c.json 2> $OUT/$c.err || { echo "$c failed"; tail -3 $OUT/$c.err; exit 1; }
   show $OUT/$c.json $c
   [ -n "$NO_SQ" ] || { timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY -d $OUT/${c}_sq -o run --output-format csv -- python3 bench.py $B > $OUT/${c}_sq.log 2>&1 || { echo "sq $c failed"; tail -3 $OUT/${c}_sq.log; exit 1; }; }
-  for pk in 0 1; do
+  [ -n "$AB" ] && for pk in 0 1; do
     XE_LIB=$PWD/gobpfld_amd/libxdpemu_tuning.so XE_SEQ_PEEK=$pk timeout -k 10 240 python bench.py $B > $OUT/${c}_peek$pk.json 2> $OUT/${c}_peek$pk.err || { echo "$c peek $pk failed"; tail -3 $OUT/${c}_peek$pk.err; exit 1; }
     show $OUT/${c}_peek$pk.json "$c peek=$pk"
   done
 done
-echo done
+find $OUT -name "*.db" -delete; du -sh $OUT; echo done

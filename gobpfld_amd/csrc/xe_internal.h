@@ -124,7 +124,8 @@ struct XeDevMap {
   uint8_t* vals;        // ARRAY memory / HASH slot values (slot cap = the nil-key slot)
   uint64_t* keys;       // HASH: (cap+1) slot records of rwords u64 words: [0] = slot state, then the
                         // zero-padded key words (one probe touches one record, one cache line)
-  uint32_t* state;      // unused on the device (host-side layout keeps separate arrays)
+  uint32_t* state;      // LRU: list_cap replicas of the stamps (pool_cap u64 words each) for the
+                        // touches of a parallel / SPEC pass (xe_interp.h lru_touch); otherwise unused
   uint32_t* count;      // HASH: number of entries (device word)
   uint32_t cap;         // HASH: power-of-two slot count
   uint32_t kwords;      // HASH: (key_size+7)/8

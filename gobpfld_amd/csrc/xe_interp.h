@@ -1965,9 +1965,16 @@ XE_DEV void lru_promote(XeLane& L, const XeDevMap& M, uint32_t v) {  // promote,
 XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_word0(M, uint64_t(slot)) >> 32); }
 // Concurrent modes: a touch (lookup hit, update) of value v by this packet — its last touch in packet order
 // is what the UsageList keeps (the runtime relinks by it, lru_finalize)
-XE_DEV int lru_touch(XeLane& L, const XeDevMap& M, uint32_t v) {
+// A hot flow's value takes an atomic max from most waves of a pass, all on one word: the parallel and
+// SPEC passes spread them over M.list_cap replicas of the stamps (in M.state, pool_cap words apart; wave w
+// uses replica w % list_cap), which the runtime folds into M.tag after the launch (xe_runtime.cpp
+// lru_tag_fold). A chain's touches (one lane per key) go to M.tag itself.
+XE_DEV int lru_touch(XeLane& L, const XeParams& P, const XeDevMap& M, uint32_t v) {
   if (L.oseq >= 0xffffu) return XE_EV_ORD;
-  xe_atomic_max64((unsigned long long*)M.tag + v, lru_stamp(L, M));
+  unsigned long long* t = (unsigned long long*)M.tag + v;
+  if (M.list_cap > 1 && P.mode != XE_MODE_CHAIN)
+    t = (unsigned long long*)M.state + uint64_t(L.wave % M.list_cap) * M.pool_cap + v;
+  xe_atomic_max64(t, lru_stamp(L, M));
   return 0;
 }
 // LRU lookup of a key (no promotion); value id or XE_NONE
@@ -2104,7 +2111,7 @@ XE_DEV int map_lookup(XeLane& L, const XeParams& P, uint32_t m, const XeReg& K, 
         // a lookup promotes (maps_hash_lru.go:70-91): in packet order the key ends up at the head as
         // often as it was touched last; the run keeps each value's last touch (packet << 16 | call) + 1
         // and the runtime moves the touched keys to the UsageList's head by it (ordered_finalize)
-        if (int e = lru_touch(L, M, v)) return e;
+        if (int e = lru_touch(L, P, M, v)) return e;
         out = XeReg{0, hv_make(M, m, v), XE_KIND_MEMPTR};
 #if XE_KEYED
         if (kid) { L.kh = out.h; L.kk = kid; }
@@ -2344,7 +2351,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     if (v == XE_NONE) {
       if (int e = lru_insert(L, M, kw, empty, v)) return e;
     } else if (xe_concurrent(P)) {
-      if (int e = lru_touch(L, M, v)) return e;  // appended + promoted, or promoted (:144-150)
+      if (int e = lru_touch(L, P, M, v)) return e;  // appended + promoted, or promoted (:144-150)
       if (int e = bm_before_write(L, P, hv_make(M, m, v))) return e;
     } else {
       lru_promote(L, M, v);

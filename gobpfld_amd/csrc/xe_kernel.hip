@@ -358,6 +358,28 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// An LRU map's stamp replicas (xe_interp.h lru_touch) into its stamps, and zeroed: one u64 per value
+// and replica read, the touched ones written
+__global__ void xe_lru_tag_fold_kernel(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r) {
+  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < pool; v += uint64_t(gridDim.x) * blockDim.x) {
+    uint64_t mx = 0;
+    for (uint32_t k = 0; k < r; k++) {
+      const uint64_t x = rep[k * uint64_t(pool) + v];
+      if (x) {
+        mx = x > mx ? x : mx;
+        rep[k * uint64_t(pool) + v] = 0;
+      }
+    }
+    if (mx > tag[v]) tag[v] = mx;
+  }
+}
+extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, hipStream_t s) {
+  if (!pool) return 0;
+  const uint32_t blocks = pool / 256 + 1 < 8192 ? pool / 256 + 1 : 8192;
+  hipLaunchKernelGGL(xe_lru_tag_fold_kernel, dim3(blocks), dim3(256), 0, s, tag, rep, pool, r);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // The one-lane replay's order log of an LRU map (xe_interp.h lru_log_push): the live values (the first
 // hdr[2] of `order`, the pool sorted by stamp, descending) oldest first as {stamp, value id}, from word 8
 __global__ void xe_lru_log_kernel(const uint64_t* tag, const uint32_t* order, const uint64_t* hdr, uint64_t* log) {

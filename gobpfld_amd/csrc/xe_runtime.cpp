@@ -52,6 +52,7 @@ extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* s
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                                     size_t* bytes, int renumber, hipStream_t s);
+extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, hipStream_t s);
 extern "C" int xe_launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log,
                                  hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -271,6 +272,15 @@ int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link
   hdr[1] = cnt ? v[cnt - 1] : XE_NONE;
   return 0;
 }
+int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, xe_stream_t) {  // xe_lru_tag_fold_kernel
+  for (uint64_t v = 0; v < pool; v++)
+    for (uint32_t k = 0; k < r; k++) {
+      uint64_t& x = rep[k * uint64_t(pool) + v];
+      if (x > tag[v]) tag[v] = x;
+      x = 0;
+    }
+  return 0;
+}
 int launch_lru_log(const uint64_t* tag, uint32_t, const uint32_t* order, const uint64_t* hdr, uint64_t* log, xe_stream_t) {
   const uint64_t cnt = hdr[2];  // xe_kernel.hip xe_lru_log_kernel: oldest first
   for (uint64_t i = 0; i < cnt; i++) {
@@ -364,6 +374,9 @@ void host_free(void* p) { if (p) (void)hipHostFree(p); }
 int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                       size_t* bytes, int renumber, xe_stream_t s) {
   return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, renumber, s);
+}
+int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, xe_stream_t s) {
+  return xe_launch_lru_tag_fold(tag, rep, pool, r, s);
 }
 int launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log, xe_stream_t s) {
   return xe_launch_lru_log(tag, pool, order, hdr, log, s);
@@ -714,6 +727,9 @@ struct HostMap {
   uint64_t n_vals = 0, n_elen = 0, n_link = 0, n_rec = 0;  // allocated elements of the device arrays
   uint64_t* d_tag = nullptr;  // QUEUE / STACK / PERF: order keys of a parallel run's appends (pool_cap)
   uint64_t n_tag = 0;         // LRU: each value's stamp (xe_interp.h lru_stamp: the UsageList as numbers)
+  uint64_t* d_trep = nullptr;   // LRU: trep_r replicas of the stamps (lru_touch in parallel / SPEC passes)
+  uint64_t n_trep = 0;
+  uint32_t trep_r = 0;
   uint64_t* d_tsnap = nullptr;  // LRU: the stamps at a parallel run's start (its touches are rolled back)
   uint64_t n_tsnap = 0;
   bool links_stale = false;     // LRU: a parallel / keyed run left only stamps (lru_relink rebuilds the links)
@@ -1100,6 +1116,10 @@ void map_free_device(HostMap& m) {
   dev_free(m.d_tag);
   m.d_tag = nullptr;
   m.n_tag = 0;
+  dev_free(m.d_trep);
+  m.d_trep = nullptr;
+  m.n_trep = 0;
+  m.trep_r = 0;
   dev_free(m.d_vsnap);
   m.d_vsnap = nullptr;
   m.n_vsnap = 0;
@@ -1148,6 +1168,10 @@ int upload_map_table(xe_vm* vm, xe_stream_t s) {
     d.rec = m.d_rec;  // PERF: event records; LRU: the one-lane replay's order log (lru_log_build)
     d.pool_cap = m.pool_cap;
     d.list_cap = m.list_cap;
+    if (m.dkind == XE_DM_LRU) {  // the stamp replicas (xe_interp.h lru_touch)
+      d.state = (uint32_t*)m.d_trep;
+      d.list_cap = m.trep_r;
+    }
     d.data_cap = m.data_cap;
     d.tag = m.d_tag;
   }
@@ -1385,6 +1409,17 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
       return -1;
   }
   if (ensure_dev(&m.d_tag, m.n_tag, m.pool_cap)) return -1;
+  if (m.dkind == XE_DM_LRU) {
+    // replicas of the stamps for the touches of parallel passes (zero between runs): 16, or as many as
+    // 256 MB hold; without them a C3-LRU pass took 7.3 ms of same-word atomics on the hot flows' stamps
+    // (0.2-0.5 ms for the same pass over a HASH table, profiles/r5/c3lru_keyed_kernel_trace.csv)
+    uint32_t r = 16;
+    while (r > 1 && uint64_t(r) * m.pool_cap * 8 > (256ull << 20)) r >>= 1;
+    if (r > 1 && (ensure_dev(&m.d_trep, m.n_trep, uint64_t(r) * m.pool_cap) ||
+                  dmemset(m.d_trep, 0, uint64_t(r) * m.pool_cap * 8, st)))
+      return -1;
+    m.trep_r = r > 1 ? r : 0;
+  }
   if (m.dkind == XE_DM_LRU) {  // stamps in UsageList order (epoch 0: every run's touches are newer)
     std::vector<uint64_t> tag(m.pool_cap, 0);
     for (uint64_t i = 0; i < n; i++) tag[i] = n - i;
@@ -2688,6 +2723,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
       if (m.nrep > 1 && fold_map(m, s)) return -1;
+      if (m.dkind == XE_DM_LRU && m.trep_r > 1 && launch_lru_tag_fold(m.d_tag, m.d_trep, m.pool_cap, m.trep_r, s)) return -1;
     }
     return 0;
   };

@@ -2287,7 +2287,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     if (P.mode == XE_MODE_PARALLEL) return XE_EV_ORD;
     uint64_t kw[XE_MAX_KEY / 8];
     bool empty = false;
-    if (int e = read_key(L, P, R2, M, kw, empty, cm2)) return e;
+    if (int e = read_key(L, P, R2, M, kw, empty, cm2, kp)) return e;
 #if XE_KEYED
     const uint64_t kid = kid_hash(m, M, kw, empty);
     if (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)
@@ -2958,7 +2958,7 @@ XE_DEV int uop_helper(XeLane& L, const XeParams& P, const XeUop& u, uint32_t cm1
   return call_helper(L, P, fn, cm1, cm2, cm3);
 }
 
-// bpf_map_lookup_elem / bpf_map_update_elem of a HASH map whose key words the per-program kernel
+// bpf_map_lookup_elem / bpf_map_update_elem of a HASH / LRU_HASH map whose key words the per-program kernel
 // built from the registers it stored into the frame (xe_jit.cpp key_shadows proves them equal to the
 // ReadRange of R2); everything else about the call is call_helper's (ids 1 and 2 are never replaced
 // in a per-program kernel: a VM with a host or nil helper runs on the interpreter).
@@ -3282,8 +3282,10 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body, Peek peek) {
 #pragma unroll 1
     for (uint32_t k = 0; k < m; k++) {
       const bool valid = lane == 0;
+      // every lane stages packet k (only lane 0 runs it): the lane state is then wave-uniform, which
+      // lets the compiler keep much of the replay's arithmetic on the scalar unit
       if (P.seq_prefetch)
-        lane_stage(L, P, valid, xe_readlane64(a, int(k)), uint32_t(xe_readlane(int(l), int(k))),
+        lane_stage(L, P, true, xe_readlane64(a, int(k)), uint32_t(xe_readlane(int(l), int(k))),
                    xe_readlane(int(f), int(k)) != 0, L.hdrbuf, int(k));
       else
         lane_reset(L, P, c0 + k, valid);

@@ -65,12 +65,12 @@ def alg_bytes_per_packet(name: str, sizes: np.ndarray) -> np.ndarray:
 ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
 
 
-PROFILE_ROUND = "r4"  # newest committed PMC passes (scripts/gpu_pmc.sh); earlier rounds' are superseded
+PROFILE_ROUNDS = ("r5", "r4", "r3")  # committed PMC passes, newest first (a newer round's file supersedes)
 
 
 def _profile(name: str, kind: str, n: int) -> tuple[dict | None, str | None]:
     """profiles/<round>/<config>_<kind>.json of this exact workload and batch size (newest round first)."""
-    for rnd in (PROFILE_ROUND, "r3"):
+    for rnd in PROFILE_ROUNDS:
         f = ROOT / "profiles" / rnd / f"{name}_{kind}.json"
         if f.exists():
             d = json.loads(f.read_text())

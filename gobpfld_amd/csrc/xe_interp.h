@@ -1293,9 +1293,6 @@ XE_DEV unsigned long long xe_lds_xchg64(XE_LP(unsigned long long) p, unsigned lo
 XE_DEV int xe_lds_add32(XE_LP(int) p, int v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
-XE_DEV void xe_lds_max64(XE_LP(unsigned long long) p, unsigned long long v) {
-  __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
 #else
 XE_DEV unsigned long long xe_lds_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
   unsigned long long o = *p;
@@ -1305,7 +1302,6 @@ XE_DEV unsigned long long xe_lds_cas64(unsigned long long* p, unsigned long long
 XE_DEV void xe_lds_add64(unsigned long long* p, unsigned long long v) { *p += v; }
 XE_DEV unsigned long long xe_lds_xchg64(unsigned long long* p, unsigned long long v) { unsigned long long o = *p; *p = v; return o; }
 XE_DEV int xe_lds_add32(int* p, int v) { int o = *p; *p += v; return o; }
-XE_DEV void xe_lds_max64(unsigned long long* p, unsigned long long v) { if (v > *p) *p = v; }
 #endif
 
 XE_DEV uint32_t acc_slot(uint64_t addr) {
@@ -1324,43 +1320,9 @@ XE_DEV void field_add(const XeLane& L, uint32_t m, uint64_t addr, int size, uint
     xe_atomic_add32(reinterpret_cast<unsigned int*>(uintptr_t(addr)), uint32_t(v));
   }
 }
-// accumulator tag = field address (48 bits) | map << 48 | size << 56; size XE_ACC_MAX: an LRU stamp
-// word whose entry holds the largest stamp of the wave's touches (wave_max_stamp)
-#define XE_ACC_MAX 0x88u
+// accumulator tag = field address (48 bits) | map << 48 | size << 56
 XE_DEV void acc_apply(const XeLane& L, unsigned long long tag, unsigned long long v) {
-  if ((tag >> 56) == XE_ACC_MAX) {
-    xe_atomic_max64(reinterpret_cast<unsigned long long*>(uintptr_t(tag & 0xffffffffffffull)), v);
-    return;
-  }
   field_add(L, uint32_t((tag >> 48) & 0xffu), tag & 0xffffffffffffull, int(tag >> 56), v);
-}
-
-// max(*p, s) for an LRU stamp word through the wave's accumulator table (the entries of wave_atomic_
-// add_field, same claim / score / take-over rules): a hot flow's touches by the wave's packets become
-// one memory-side atomic when the entry is flushed or taken over, instead of one per touch
-XE_DEV void wave_max_stamp(XeLane& L, unsigned long long* p, unsigned long long st) {
-  XePend* acc = L.pend;
-  const uint64_t addr = uint64_t(uintptr_t(p));
-  const unsigned long long tag = addr | (uint64_t(XE_ACC_MAX) << 56);
-  const uint32_t k = acc_slot(addr);
-  XE_LP(unsigned long long) tp = (XE_LP(unsigned long long))&acc->tag[k];
-  XE_LP(int) sp = (XE_LP(int))&acc->score[k];
-  const unsigned long long t = *tp;
-  if (t == 0) {
-    if (xe_lds_cas64(tp, 0ull, tag) == 0) *sp = 1;
-  } else if (t != tag) {
-    if (xe_lds_add32(sp, -1) <= 1 && xe_lds_cas64(tp, t, tag) == t) {
-      const unsigned long long old = xe_lds_xchg64((XE_LP(unsigned long long))&acc->sum[k], 0ull);
-      *sp = 2;
-      if (old) acc_apply(L, t, old);
-    }
-  }
-  if (*tp == tag) {
-    xe_lds_max64((XE_LP(unsigned long long))&acc->sum[k], st);
-    if (t == tag) xe_lds_add32(sp, 1);
-    return;
-  }
-  xe_atomic_max64(p, st);
 }
 
 #if XE_PAIR_ADDS
@@ -2004,10 +1966,10 @@ XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_
 // Concurrent modes: a touch (lookup hit, update) of value v by this packet — its last touch in packet order
 // is what the UsageList keeps (the runtime relinks by it, lru_finalize)
 // A hot flow's value takes an atomic max from most waves of a pass, all on one word: the parallel and
-// SPEC passes collect each wave's touches of a word in its accumulator table (wave_max_stamp) and spread
-// what reaches memory over M.list_cap replicas of the stamps (in M.state, pool_cap words apart; wave w
-// uses replica w % list_cap), which the runtime folds into M.tag after the launch (xe_runtime.cpp
-// lru_tag_fold). A chain's touches (one lane per key) go to M.tag itself.
+// SPEC passes skip the touches that cannot raise the word and spread the rest over M.list_cap replicas
+// of the stamps (in M.state, pool_cap words apart; wave w uses replica w % list_cap), which the runtime
+// folds into M.tag after the launch (xe_runtime.cpp lru_tag_fold). A chain's touches (one lane per key)
+// go to M.tag itself.
 XE_DEV int lru_touch(XeLane& L, const XeParams& P, const XeDevMap& M, uint32_t v) {
   if (L.oseq >= 0xffffu) return XE_EV_ORD;
   unsigned long long* t = (unsigned long long*)M.tag + v;
@@ -2016,7 +1978,11 @@ XE_DEV int lru_touch(XeLane& L, const XeParams& P, const XeDevMap& M, uint32_t v
     return 0;
   }
   if (M.list_cap > 1) t = (unsigned long long*)M.state + uint64_t(L.wave % M.list_cap) * M.pool_cap + v;
-  wave_max_stamp(L, t, lru_stamp(L, M));
+  // a hot flow's word almost always holds a newer stamp already (the waves walk the batch in step, so a
+  // touch is rarely the newest so far): read it first. A stale read from this CU's cache is never too
+  // new (stamps only grow), so a skipped atomic could never have raised the word.
+  const unsigned long long st = lru_stamp(L, M);
+  if (*(XE_GP(const unsigned long long))t < st) xe_atomic_max64(t, st);
   return 0;
 }
 // LRU lookup of a key (no promotion); value id or XE_NONE

@@ -138,7 +138,7 @@ struct XeDevMap {
   // LRU_HASH / QUEUE / STACK / PERF_EVENT_ARRAY (ordered maps; the general lane model only)
   //   LRU:  keys = slot records ([0] = state | value id << 32), vals = value pool (pool_cap values),
   //         link = prev/next value ids (UsageList as a linked list), elen = value length (0: nil backing),
-  //         hdr = {head (MRU), tail (LRU), count, next value id}, tag = stamps; the one-lane replay's
+  //         hdr = {head (MRU), tail (LRU), count, next value id, any nil-backed value, stamp base, touch counter}, tag = stamps; the one-lane replay's
   //         order log in rec, data_cap entries (xe_interp.h lru_log_push)
   //   LIST: vals = element pool, elen = element length, link = the list (ring of list_cap ids for a
   //         queue), hdr = {head, count, next element id, 0, is_stack}

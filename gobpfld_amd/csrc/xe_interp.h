@@ -1078,7 +1078,10 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
   if (M.kind == XE_DM_LRU) {
     const uint64_t vid = hv_slot(h);
     B.base = M.vals + vid * M.value_size;
-    B.len = int64_t(((XE_GP(const uint32_t))M.elen)[vid]);
+    // header word 4: some value may have a nil backing (an update whose value pointer was unreadable);
+    // until then every value is value_size long and its length word is not read (one dependent load
+    // less per value access)
+    B.len = ((XE_GP(const uint64_t))M.hdr)[4] ? int64_t(((XE_GP(const uint32_t))M.elen)[vid]) : int64_t(M.value_size);
     return true;
   }
 #endif
@@ -2367,6 +2370,7 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
     }
     uint8_t* dst = M.vals + uint64_t(v) * M.value_size;
     ((XE_GP(uint32_t))M.elen)[v] = ve ? 0u : M.value_size;
+    if (ve) *map_hdr(M, 4) = 1;  // a nil-backed value exists (bmem_resolve reads lengths from now on)
     if (!ve) ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t i, uint8_t b) { ((XE_GP(uint8_t))dst)[i] = b; }, cm3);
     return helper_errno_result(L, 0);
   }

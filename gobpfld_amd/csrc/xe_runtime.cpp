@@ -1392,6 +1392,8 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
       if (!m.d_keys && dev_alloc((void**)&m.d_keys, rec.size() * 8)) return -1;
       if (h2d(m.d_keys, rec.data(), rec.size() * 8, st)) return -1;
       hdr[0] = n ? 0 : XE_NONE; hdr[1] = n ? n - 1 : XE_NONE; hdr[2] = n; hdr[3] = n;
+      for (uint64_t i = 0; i < n && !hdr[4]; i++)  // a value not value_size long (xe_interp.h bmem_resolve)
+        hdr[4] = elen[i] != vs ? 1 : 0;
       hdr[5] = vm->lru_epoch << 48;  // the stamp base of the run in progress (xe_interp.h lru_stamp)
       hdr[6] = 0;
     } else {  // QUEUE / STACK: element i is Values[i]; the list starts at 0

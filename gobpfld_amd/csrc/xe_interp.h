@@ -1974,6 +1974,9 @@ XE_DEV uint32_t lru_vid(const XeDevMap& M, int64_t slot) { return uint32_t(hash_
 // folds into M.tag after the launch (xe_runtime.cpp lru_tag_fold). A chain's touches (one lane per key)
 // go to M.tag itself.
 XE_DEV int lru_touch(XeLane& L, const XeParams& P, const XeDevMap& M, uint32_t v) {
+#if defined(XE_DEBUG_NO_LRU_TOUCH)  // cost experiments only: touches dropped (the UsageList is wrong)
+  return 0;
+#endif
   if (L.oseq >= 0xffffu) return XE_EV_ORD;
   unsigned long long* t = (unsigned long long*)M.tag + v;
   if (P.mode == XE_MODE_CHAIN) {

@@ -1083,7 +1083,8 @@ uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc, bool hash) {
 // vals += the replicas (replicas := 0); a HASH map only over the slots that hold or held an entry
 int fold_map(HostMap& m, xe_stream_t s) {
   const bool hash = m.dkind == XE_DM_HASH && m.def.value_size > 0;
-  return launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, m.vals_alloc / 8, hash ? m.d_keys : nullptr,
+  const uint64_t words = m.dkind == XE_DM_LRU ? (uint64_t(m.pool_cap) * m.def.value_size + 7) / 8 : m.vals_alloc / 8;
+  return launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, words, hash ? m.d_keys : nullptr,
                          hash ? xe_hash_rwords(m.kwords) : 0, hash ? m.def.value_size : 8, m.cap, s);
 }
 
@@ -1539,13 +1540,26 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       vm->staged_slot = -1;  // the device values change under the staged snapshots
       if (map_upload(vm, m)) return fail(vm, XE_ERR_DEVICE, "map upload");
     }
-    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : m.vals_bytes;
-    uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH) ? choose_nrep(live, m.vals_alloc, m.dkind == XE_DM_HASH) : 1u;
+    // LRU_HASH value pools take replicas like an ARRAY region: a hot flow's adds otherwise meet on one
+    // word from every wave (C3-LRU keyed: 5.3 of a 7.5 ms batch were its map adds, profiles/r5/lru_ab.txt)
+    const bool lru = m.dkind == XE_DM_LRU;
+    const uint64_t region = lru ? ((uint64_t(m.pool_cap) * m.def.value_size + 7) & ~uint64_t(7)) : m.vals_alloc;
+    if (lru && ((region + 255) & ~uint64_t(255)) != m.rep_stride) {  // first run, or the pool grew
+      dev_free(m.d_rep);
+      m.d_rep = nullptr;
+      m.nrep = 1;
+      m.nrep_fixed = false;
+      m.rep_stride = (region + 255) & ~uint64_t(255);
+      vm->jit_idx = -1;  // the stride is compiled into the per-program kernel
+    }
+    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : lru ? region : m.vals_bytes;
+    uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH || (lru && region))
+                        ? choose_nrep(live, region, m.dkind == XE_DM_HASH) : 1u;
     // the replica count is compiled into the per-program kernel: once chosen it stays while its fold stays
     // bounded, so a table that grows over a stream of batches (C3-learn: 1 -> 5 MB live, 16 -> 4 replicas
     // by the tiers) does not recompile mid-stream (a 9 s hiprtc compile in the measured stream)
     if (m.nrep_fixed && want != m.nrep && !xe_tuning_env("XE_NREP") &&
-        (m.nrep == 1 || nrep_bounded(m.nrep, live, m.vals_alloc, m.dkind == XE_DM_HASH)))
+        (m.nrep == 1 || nrep_bounded(m.nrep, live, region, m.dkind == XE_DM_HASH)))
       want = m.nrep;
     m.nrep_fixed = true;
     if (want != m.nrep) {  // replicas are all zero between runs (the fold clears them)

@@ -1549,10 +1549,10 @@ int prepare_run(xe_vm* vm, xe_stream_t s) {
       m.d_rep = nullptr;
       m.nrep = 1;
       m.nrep_fixed = false;
-      m.rep_stride = (region + 255) & ~uint64_t(255);
-      vm->jit_idx = -1;  // the stride is compiled into the per-program kernel
+      m.rep_stride = (region + 255) & ~uint64_t(255);  // (read from the descriptor table: no recompile)
     }
-    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : lru ? region : m.vals_bytes;
+    // (an LRU map's live bytes are not tracked on the host: the tier for a small one, bounded by the pool)
+    const uint64_t live = m.dkind == XE_DM_HASH ? uint64_t(m.live) * m.def.value_size : lru ? 0 : m.vals_bytes;
     uint32_t want = (m.dkind == XE_DM_ARRAY || m.dkind == XE_DM_HASH || (lru && region))
                         ? choose_nrep(live, region, m.dkind == XE_DM_HASH) : 1u;
     // the replica count is compiled into the per-program kernel: once chosen it stays while its fold stays

@@ -125,10 +125,12 @@ _SIGS = {
     "prepare": (C.c_int, [P]),
     "debug_set_schedule": (C.c_int, [P, C.c_uint32]),
     "debug_set_lru_epoch": (C.c_int, [P, C.c_uint64]),
+    "debug_map_pool": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "set_kernel_cache": (C.c_int, [C.c_char_p]),
     "kernel_source": (C.c_int, [P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "compile_kernel_source": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     "kernel_object_name": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "kernel_cache_stats": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "map_values_bytes": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint64)]),
     "map_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
     "map_apply_delta": (C.c_int, [P, C.c_int32, C.c_uint32, P, P]),
@@ -165,8 +167,9 @@ HEADER_SYMBOLS = [
     "xe_device_count", "xe_shard_check", "xe_epoch_begin", "xe_epoch_end", "xe_map_state_bytes", "xe_map_state_export",
     "xe_map_state_import",
     "xe_multi_create", "xe_multi_destroy", "xe_run_batch_multi", "xe_multi_last_error", "xe_debug_set_schedule",
-    "xe_debug_set_lru_epoch",
+    "xe_debug_set_lru_epoch", "xe_debug_map_pool",
     "xe_set_kernel_cache", "xe_kernel_source", "xe_compile_kernel_source", "xe_kernel_object_name",
+    "xe_kernel_cache_stats",
     "xe_cancel", "xe_trace_config", "xe_trace_read", "xe_set_helper", "xe_reset_helper",
 ]
 IO_HEADER_SYMBOLS = ["xe_pcap_header", "xe_pcap_count", "xe_pcap_fill", "xe_pcap_pack"]  # include/xdpemu_io.h

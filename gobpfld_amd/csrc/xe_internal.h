@@ -91,12 +91,14 @@ XE_HD int uop_size(const XeUop& u) { return 1 << ((u.fl >> 4) & 3); }
 #define XE_H_QVAL 7u    // QUEUE / STACK element (slot = element id) or PERF event (slot = event index)
 #define XE_H_MAX_MAPS 63
 #define XE_H_SLOT_BITS 23
-// A HASH / LRU_HASH map whose slots (value ids) do not fit 23 bits is a "big map" (at most 4, and then
-// at most 31 maps in the VM): a value handle of slot s >= 2^23 carries map field
-// XE_H_BIG + 8 * j + (s >> 23) for big map j, so slots up to 2^26 (MaxEntries up to 16M at half load)
-// stay one 32-bit handle (xe_interp.h hv_make / hv_map / hv_slot)
+// A HASH / LRU_HASH map whose slots (value ids) do not fit 23 bits is a "big map" (and then the VM holds
+// at most 31 maps): the 32 map-field values XE_H_BIG..63 are shared out among the big maps, each taking
+// a run of fields [base, base + f) with f * 2^23 >= its slots (its value-id pool for an LRU map), and a
+// value handle of slot s carries map field XE_H_BIG + base + (s >> 23), so up to 2^28 slots over all big
+// maps stay one 32-bit handle — one map of up to 2^27 slots (MaxEntries up to 2^27) and others beside it
+// (xe_interp.h hv_make / hv_map / hv_slot; xe_runtime.cpp xe_add_map hands the fields out)
 #define XE_H_BIG 32u
-#define XE_H_BIG_MAPS 4u
+#define XE_H_BIG_FIELDS 32u
 XE_HD uint32_t xe_h_make(uint32_t cls, uint32_t map, uint32_t slot) {
   return (cls << XE_H_CLS_SHIFT) | (map << XE_H_SLOT_BITS) | slot;
 }
@@ -118,8 +120,8 @@ struct XeDevMap {
   uint32_t key_size;
   uint32_t value_size;
   uint32_t max_entries;
-  uint32_t big;         // HASH / LRU_HASH with slots past the handle's 23-bit slot field: 1 + its big-map
-                        // number (value handles, xe_interp.h hv_make), 0 otherwise
+  uint32_t big;         // HASH / LRU_HASH with slots past the handle's 23-bit slot field: 1 + the first of
+                        // its big-map fields (value handles, xe_interp.h hv_make), 0 otherwise
   uint64_t vals_bytes;  // ARRAY: value_size*max_entries; HASH: (cap+1)*value_size
   uint8_t* vals;        // ARRAY memory / HASH slot values (slot cap = the nil-key slot)
   uint64_t* keys;       // HASH: (cap+1) slot records of rwords u64 words: [0] = slot state, then the
@@ -372,7 +374,8 @@ struct XeParams {
   const xe_desc* desc;
   uint32_t n;
   uint32_t nmaps;         // len(vm.Maps) - 1
-  uint8_t bigmap[XE_H_BIG_MAPS];  // big map j's map index (value handles with map field >= XE_H_BIG)
+  uint8_t bigmap[XE_H_BIG_FIELDS];  // map field XE_H_BIG + f: the big map's index, and the field's place
+  uint8_t bigoff[XE_H_BIG_FIELDS];  // in that map's run (slot bits 23 and up of the handle)
   xe_result* results;
   uint32_t* verdicts;
   xe_regs* regs;
@@ -418,6 +421,7 @@ struct XeParams {
   // packet's pop takes the element at its rank popbase[i] among the batch's pops in packet order.
   XeListRun* list;
   uint32_t pop_mode;
+  uint32_t pop_map;       // pop_mode 2: the one list the batch pops (the ranks count its pops only)
   uint32_t* popflag;
   const uint32_t* popbase;
   // helper table (xe_set_helper): bit id of host[] = a host function, of nil[] = a nil entry

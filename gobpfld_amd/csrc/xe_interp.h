@@ -883,15 +883,15 @@ XE_DEV XeDevMap map_desc(const XeLane& L, uint32_t m) {
 // HASH / LRU_HASH value handles (xe_internal.h XE_H_BIG): slot (or value id) s of map m, and back
 XE_DEV uint32_t hv_make(const XeDevMap& M, uint32_t m, uint32_t s) {
   if (s < (1u << XE_H_SLOT_BITS) || !M.big) return xe_h_make(XE_H_HASH, m, s);
-  return xe_h_make(XE_H_HASH, XE_H_BIG + 8u * (M.big - 1u) + (s >> XE_H_SLOT_BITS), s & ((1u << XE_H_SLOT_BITS) - 1u));
+  return xe_h_make(XE_H_HASH, XE_H_BIG + (M.big - 1u) + (s >> XE_H_SLOT_BITS), s & ((1u << XE_H_SLOT_BITS) - 1u));
 }
 XE_DEV uint32_t hv_map(const XeParams& P, uint32_t h) {
   const uint32_t m = xe_h_map(h);
-  return m >= XE_H_BIG ? uint32_t(P.bigmap[(m - XE_H_BIG) >> 3]) : m;
+  return m >= XE_H_BIG ? uint32_t(P.bigmap[m - XE_H_BIG]) : m;
 }
-XE_DEV uint32_t hv_slot(uint32_t h) {
+XE_DEV uint32_t hv_slot(const XeParams& P, uint32_t h) {
   const uint32_t m = xe_h_map(h);
-  return (m >= XE_H_BIG ? ((m - XE_H_BIG) & 7u) << XE_H_SLOT_BITS : 0u) | xe_h_slot(h);
+  return (m >= XE_H_BIG ? uint32_t(P.bigoff[m - XE_H_BIG]) << XE_H_SLOT_BITS : 0u) | xe_h_slot(h);
 }
 
 XE_DEV uint64_t fp_bits(const XeDevMap& M, bool array, int64_t off, int size) {
@@ -1076,7 +1076,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
     return true;
   }
   if (M.kind == XE_DM_LRU) {
-    const uint64_t vid = hv_slot(h);
+    const uint64_t vid = hv_slot(P, h);
     B.base = M.vals + vid * M.value_size;
     // header word 4: some value may have a nil backing (an update whose value pointer was unreadable);
     // until then every value is value_size long and its length word is not read (one dependent load
@@ -1085,7 +1085,7 @@ XE_DEV bool bmem_resolve(const XeLane& L, const XeParams& P, uint32_t h, XeBMem&
     return true;
   }
 #endif
-  uint32_t slot = hv_slot(h);
+  uint32_t slot = hv_slot(P, h);
   B.base = M.vals + uint64_t(slot) * M.value_size;
   B.len = (uint32_t(((XE_GP(const uint64_t))M.keys)[uint64_t(slot) * M.rwords]) & XE_SLOT_VLEN0) ? 0 : int64_t(M.value_size);
   return true;
@@ -1101,12 +1101,12 @@ XE_DEV int key_touch_mem(XeLane& L, const XeParams& P, uint32_t h, const XeBMem&
   if (B.array) return key_touch_array(L, P, B.map, M, off, size, write, dkey);
   if (M.kind == XE_DM_LRU && xe_h_cls(h) == XE_H_HASH) {  // an LRU value: the key of its slot record
     if (h == L.kh) return key_touch(L, P, L.kk, write, dkey);
-    const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(hv_slot(h)) + 2];
+    const uint32_t slot = ((XE_GP(const uint32_t))M.link)[4 * uint64_t(hv_slot(P, h)) + 2];
     return key_touch(L, P, kid_slot(B.map, M, slot), write, dkey);
   }
   // queue / stack elements and perf events follow packet order: a write to one is never keyed
   if (M.kind != XE_DM_HASH) return write ? XE_EV_ORD : 0;
-  return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, hv_slot(h)), write, dkey);
+  return key_touch(L, P, h == L.kh ? L.kk : kid_slot(B.map, M, hv_slot(P, h)), write, dkey);
 }
 #endif
 
@@ -2003,11 +2003,36 @@ XE_DEV void lru_erase(const XeDevMap& M, uint32_t v) {
   ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_TOMB;
   *map_hdr(M, 2) -= 1;
 }
+// The one-lane replay reuses evicted value ids. A packet may still hold a pointer to the value it evicted
+// (Go keeps that ByteMemory alive), so an id freed by packet p is handed out again only to a later packet:
+// a FIFO of freed ids in order-log words 2 (first) / 3 (last), linked through the freed entries' link
+// words 0 (next) and 1 (the freeing packet), which only lru_relink's host-side list uses (rebuilt from the
+// stamps after the run); the runtime empties it with every seed of the log (xe_lru_log_kernel). Without
+// it the pool only grew: a stream of evicting replays climbed to the value ids the handles can name.
+XE_DEV void lru_free_push(const XeLane& L, const XeDevMap& M, uint32_t v) {
+  XE_GP(uint64_t) lg = (XE_GP(uint64_t))M.rec;
+  *lru_link(M, v, 0) = XE_NONE;
+  *lru_link(M, v, 1) = L.pidx;
+  if (lg[3] == XE_NONE) lg[2] = v;
+  else *lru_link(M, uint32_t(lg[3]), 0) = v;
+  lg[3] = v;
+}
+XE_DEV uint32_t lru_free_pop(const XeLane& L, const XeDevMap& M) {
+  XE_GP(uint64_t) lg = (XE_GP(uint64_t))M.rec;
+  const uint64_t h = lg[2];
+  if (h == XE_NONE || *lru_link(M, uint32_t(h), 1) >= L.pidx) return XE_NONE;
+  lg[2] = *lru_link(M, uint32_t(h), 0);
+  if (lg[2] == XE_NONE) lg[3] = XE_NONE;
+  return uint32_t(h);
+}
 XE_DEV int lru_insert(XeLane& L, const XeDevMap& M, const uint64_t* kw, bool empty, uint32_t& v) {
-  const uint64_t nv = *map_hdr(M, 3);
-  if (nv >= M.pool_cap) return XE_EV_CAP;
-  v = uint32_t(nv);
-  *map_hdr(M, 3) = nv + 1;
+  v = lru_free_pop(L, M);
+  if (v == XE_NONE) {
+    const uint64_t nv = *map_hdr(M, 3);
+    if (nv >= M.pool_cap) return XE_EV_CAP;
+    v = uint32_t(nv);
+    *map_hdr(M, 3) = nv + 1;
+  }
   const int64_t slot = hash_insert_new(M, kw, empty);
   ((XE_GP(uint64_t))M.keys)[uint64_t(slot) * M.rwords] = XE_SLOT_FULL | (uint64_t(v) << 32);
   *lru_link(M, v, 2) = uint32_t(slot);
@@ -2034,13 +2059,15 @@ XE_DEV uint32_t list_at(const XeDevMap& M, uint64_t i) {  // Values[i] in Go sli
 // stack position: pushes land on top) assumes no push came before and records the packet in sens, and
 // the host replays the batch in order when a push did (push[m] < sens[m]).
 XE_DEV bool list_par(const XeParams& P) { return P.list && P.mode == XE_MODE_PARALLEL; }
-XE_DEV uint64_t list_pops_before(const XeLane& L, const XeParams& P) {
-  return uint64_t(P.pop_mode == 2 ? P.popbase[L.pidx] : 0u) + L.npops;
+// (only the popped list loses elements: a peek or lookup of another list sees its start contents)
+XE_DEV uint64_t list_pops_before(const XeLane& L, const XeParams& P, uint32_t m) {
+  if (P.pop_mode != 2 || m != P.pop_map) return 0;
+  return uint64_t(P.popbase[L.pidx]) + L.npops;
 }
 XE_DEV void list_mark_sens(const XeLane& L, const XeParams& P, uint32_t m) { xe_atomic_max32(&P.list->sens[m], L.pidx + 1u); }
 // position (Go slice index) of Values[kv] for the lane's packet; false: out of range
 XE_DEV bool list_pos(const XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, int64_t kv, int64_t& pos) {
-  const int64_t q = int64_t(list_pops_before(L, P)), cnt0 = int64_t(P.list->cnt0[m]);
+  const int64_t q = int64_t(list_pops_before(L, P, m)), cnt0 = int64_t(P.list->cnt0[m]);
   if (!*map_hdr(M, 4)) {  // queue: front = start position q
     if (kv < 0) return false;
     if (q + kv >= cnt0) { list_mark_sens(L, P, m); return false; }
@@ -2316,9 +2343,20 @@ XE_DEV int helper_update(XeLane& L, const XeParams& P, uint32_t cm1 = XE_CM_ALL,
       if (tail == XE_NONE) return XE_EV_PANIC | XE_P_INDEX;  // UsageList[len-1] of an empty list
       if (int e = bm_before_write(L, P, hv_make(M, m, tail))) return e;
       lru_erase(M, tail);  // evicted before the value is checked
+      lru_free_push(L, M, tail);
     }
+#if XE_KEYED
+    // a new key whose value check fails: in the reference the eviction of a full map has already happened
+    // (:113-119 before :134-137) and stays. Keyed batches decide evictions in the build from the logged
+    // inserts, and this packet logs none, so whether the map is full here depends on the other packets'
+    // inserts: the batch replays in order
+    if (v == XE_NONE && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN) && !XE_ISPTR(R3.t)) return XE_EV_ORD;
+#endif
     if (!XE_ISPTR(R3.t)) return helper_errno_result(L, -14);
     int ve = ptr_read_range(L, P, R3, int64_t(M.value_size), [&](int64_t, uint8_t) {}, cm3);
+#if XE_KEYED
+    if (XE_IS_PANIC(ve) && v == XE_NONE && (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)) return XE_EV_ORD;
+#endif
     if (XE_IS_PANIC(ve)) return ve;
 #if XE_KEYED
     if (P.mode == XE_MODE_SPEC || P.mode == XE_MODE_CHAIN)
@@ -2584,7 +2622,7 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       if (xe_concurrent(P)) {
         // the count pass flags the packet and stops it; the next pass pops the element at the packet's
         // rank (one pop per packet: a second one replays the batch in order)
-        if (!list_par(P) || P.pop_mode == 0 || L.npops || (P.pop_mode == 2 && !P.popflag[L.pidx])) return XE_EV_ORD;
+        if (!list_par(P) || P.pop_mode == 0 || L.npops || (P.pop_mode == 2 && (!P.popflag[L.pidx] || m != P.pop_map))) return XE_EV_ORD;
         if (P.pop_mode == 1) {
           P.popflag[L.pidx] = 1u;
           xe_atomic_or64(&P.list->popmask, 1ull << m);

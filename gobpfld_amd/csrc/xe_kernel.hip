@@ -62,7 +62,9 @@ __global__ void xe_sum_kernel(C* acc, const C* in, uint64_t n) {
 extern "C" __global__ void xe_rep_fold_kernel(unsigned long long* __restrict__ vals, unsigned long long* __restrict__ rep,
                                               uint64_t stride_words, uint32_t nrep, uint64_t nwords,
                                               const unsigned long long* __restrict__ recs, uint32_t rwords, uint32_t vsize,
-                                              uint32_t cap) {
+                                              uint32_t cap, const unsigned long long* __restrict__ lim) {
+  // an LRU value pool: only the value ids handed out so far (header word 3) can hold replica adds
+  if (lim) nwords = nwords < (lim[3] * vsize + 7) / 8 ? nwords : (lim[3] * vsize + 7) / 8;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nwords; i += uint64_t(gridDim.x) * blockDim.x) {
     if (recs) {
       const uint64_t s0 = 8 * i / vsize, s1 = (8 * i + 7) / vsize;
@@ -360,8 +362,9 @@ extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, 
 
 // An LRU map's stamp replicas (xe_interp.h lru_touch) into its stamps, and zeroed: one u64 per value
 // and replica read, the touched ones written
-__global__ void xe_lru_tag_fold_kernel(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r) {
-  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < pool; v += uint64_t(gridDim.x) * blockDim.x) {
+__global__ void xe_lru_tag_fold_kernel(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr) {
+  const uint64_t n = hdr[3] < pool ? hdr[3] : pool;  // the value ids handed out so far
+  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < n; v += uint64_t(gridDim.x) * blockDim.x) {
     uint64_t mx = 0;
     for (uint32_t k = 0; k < r; k++) {
       const uint64_t x = rep[k * uint64_t(pool) + v];
@@ -373,10 +376,11 @@ __global__ void xe_lru_tag_fold_kernel(uint64_t* tag, uint64_t* rep, uint32_t po
     if (mx > tag[v]) tag[v] = mx;
   }
 }
-extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, hipStream_t s) {
+extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr,
+                                      hipStream_t s) {
   if (!pool) return 0;
   const uint32_t blocks = pool / 256 + 1 < 8192 ? pool / 256 + 1 : 8192;
-  hipLaunchKernelGGL(xe_lru_tag_fold_kernel, dim3(blocks), dim3(256), 0, s, tag, rep, pool, r);
+  hipLaunchKernelGGL(xe_lru_tag_fold_kernel, dim3(blocks), dim3(256), 0, s, tag, rep, pool, r, hdr);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -392,6 +396,7 @@ __global__ void xe_lru_log_kernel(const uint64_t* tag, const uint32_t* order, co
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     log[0] = 0;
     log[1] = cnt;
+    log[2] = log[3] = 0xffffffffull;  // no freed value ids (xe_interp.h lru_free_push)
   }
 }
 extern "C" int xe_launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log,
@@ -497,10 +502,12 @@ extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, cons
   return 0;
 }
 extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords,
-                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, hipStream_t s) {
+                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, const void* lim,
+                                  hipStream_t s) {
   uint32_t blocks = uint32_t(nwords / 256 + 1);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(xe_rep_fold_kernel, dim3(blocks), dim3(256), 0, s, (unsigned long long*)vals, (unsigned long long*)rep,
-                     stride_words, nrep, nwords, (const unsigned long long*)recs, rwords, vsize, cap);
+                     stride_words, nrep, nwords, (const unsigned long long*)recs, rwords, vsize, cap,
+                     (const unsigned long long*)lim);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -35,7 +35,7 @@ extern "C" int xe_launch_delta(const void* cur, const void* snap, void* out, uin
 extern "C" int xe_launch_apply_delta(void* cur, const void* snap, const void* delta, uint64_t bytes, uint32_t lane,
                                      hipStream_t s);
 extern "C" int xe_launch_rep_fold(void* vals, void* rep, uint64_t stride_words, uint32_t nrep, uint64_t nwords,
-                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, hipStream_t s);
+                                  const void* recs, uint32_t rwords, uint32_t vsize, uint32_t cap, const void* lim, hipStream_t s);
 extern "C" int xe_launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, hipStream_t s);
 extern "C" int xe_launch_prologue(const void* const* src, void* const* dst, const uint64_t* words, uint32_t nseg,
                                   void* zero, uint64_t zero_words, hipStream_t s);
@@ -52,7 +52,7 @@ extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* s
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                                     size_t* bytes, int renumber, hipStream_t s);
-extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, hipStream_t s);
+extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr, hipStream_t s);
 extern "C" int xe_launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log,
                                  hipStream_t s);
 extern "C" int xe_jit_launch(void* fn, const XeParams* P, uint32_t blocks, uint32_t threads, hipStream_t s);
@@ -154,10 +154,11 @@ int launch_prologue(const void* const* src, void* const* dst, const uint64_t* wo
   return 0;
 }
 int launch_rep_fold(void* vals, void* rep, uint64_t sw, uint32_t nrep, uint64_t nw, const void* recs, uint32_t rwords,
-                    uint32_t vsize, uint32_t cap, xe_stream_t) {
+                    uint32_t vsize, uint32_t cap, const void* lim, xe_stream_t) {
   uint64_t* v = (uint64_t*)vals;
   uint64_t* r = (uint64_t*)rep;
   const uint64_t* rc = (const uint64_t*)recs;
+  if (lim) nw = std::min<uint64_t>(nw, (((const uint64_t*)lim)[3] * vsize + 7) / 8);
   for (uint64_t i = 0; i < nw; i++) {
     if (rc) {  // xe_kernel.hip xe_rep_fold_kernel: only the words of slots that hold or held an entry
       const uint64_t s0 = 8 * i / vsize, s1 = (8 * i + 7) / vsize;
@@ -272,8 +273,8 @@ int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link
   hdr[1] = cnt ? v[cnt - 1] : XE_NONE;
   return 0;
 }
-int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, xe_stream_t) {  // xe_lru_tag_fold_kernel
-  for (uint64_t v = 0; v < pool; v++)
+int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr, xe_stream_t) {  // xe_lru_tag_fold_kernel
+  for (uint64_t v = 0; v < std::min<uint64_t>(pool, hdr[3]); v++)
     for (uint32_t k = 0; k < r; k++) {
       uint64_t& x = rep[k * uint64_t(pool) + v];
       if (x > tag[v]) tag[v] = x;
@@ -290,6 +291,7 @@ int launch_lru_log(const uint64_t* tag, uint32_t, const uint32_t* order, const u
   }
   log[0] = 0;
   log[1] = cnt;
+  log[2] = log[3] = XE_NONE;  // no freed value ids (xe_interp.h lru_free_push)
   return 0;
 }
 int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t) {
@@ -344,8 +346,8 @@ int launch_apply_delta(void* c, const void* sn, const void* d, uint64_t b, uint3
   return xe_launch_apply_delta(c, sn, d, b, lane, s);
 }
 int launch_rep_fold(void* v, void* r, uint64_t sw, uint32_t nrep, uint64_t nw, const void* recs, uint32_t rwords, uint32_t vsize,
-                    uint32_t cap, xe_stream_t s) {
-  return xe_launch_rep_fold(v, r, sw, nrep, nw, recs, rwords, vsize, cap, s);
+                    uint32_t cap, const void* lim, xe_stream_t s) {
+  return xe_launch_rep_fold(v, r, sw, nrep, nw, recs, rwords, vsize, cap, lim, s);
 }
 int launch_delta_sum(void* acc, const void* in, uint64_t bytes, uint32_t lane, xe_stream_t s) {
   return xe_launch_delta_sum(acc, in, bytes, lane, s);
@@ -375,8 +377,8 @@ int launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link
                       size_t* bytes, int renumber, xe_stream_t s) {
   return xe_launch_lru_relink(tag, pool, cnt, link, hdr, scratch, bytes, renumber, s);
 }
-int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, xe_stream_t s) {
-  return xe_launch_lru_tag_fold(tag, rep, pool, r, s);
+int launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr, xe_stream_t s) {
+  return xe_launch_lru_tag_fold(tag, rep, pool, r, hdr, s);
 }
 int launch_lru_log(const uint64_t* tag, uint32_t pool, const uint32_t* order, const uint64_t* hdr, uint64_t* log, xe_stream_t s) {
   return xe_launch_lru_log(tag, pool, order, hdr, log, s);
@@ -665,17 +667,20 @@ uint32_t next_pow2(uint64_t v) {
   return p;
 }
 
-// Slot count of a device hash table: a power of two >= 2 x MaxEntries (at most half full), or, when
-// that no longer fits the 23-bit slot field of a value handle (xe_h_make), the largest table that does
-// (2^22 slots; probes run longer above half load, every entry still has a slot: MaxEntries <= cap).
-uint32_t hash_cap(uint32_t max_entries) {
+// Slot count of a device hash table: a power of two >= 2 x MaxEntries (at most half full), or, above
+// kHashCapMax, kHashCapMax itself (probes run longer above half load; every entry still has a slot:
+// MaxEntries <= cap). kHashCapMax + 1 slots take 17 of the 32 big-map handle fields (xe_internal.h
+// XE_H_BIG), so one such table leaves room for other big maps beside it.
+constexpr uint64_t kHashCapMax = 1ull << 27;
+uint64_t hash_cap(uint64_t max_entries) {
   uint64_t mult = 2;
   if (const char* e = xe_tuning_env("XE_HASH_CAPX")) mult = uint64_t(std::max(2, atoi(e)));  // A/B: sparser tables
-  uint32_t cap = next_pow2(uint64_t(max_entries) * mult);
-  const uint32_t lim = 1u << (XE_H_SLOT_BITS + 2);  // slots of a big map's value handles (xe_internal.h XE_H_BIG)
-  if (cap > lim && max_entries <= lim) cap = lim;
+  uint64_t cap = next_pow2(max_entries * mult);
+  if (cap > kHashCapMax && max_entries <= kHashCapMax) cap = kHashCapMax;
   return cap;
 }
+// big-map handle fields (2^23 slots each, xe_internal.h XE_H_BIG) that n slots / value ids need
+uint32_t big_fields(uint64_t n) { return uint32_t((n + (1ull << XE_H_SLOT_BITS) - 1) >> XE_H_SLOT_BITS); }
 
 constexpr uint32_t kAsyncDepth = 3;
 constexpr uint32_t kKeyedBackoff = 8;  // order-dependent batches that skip the keyed path after a refusal  // pipelined batches in flight per VM (xe_run_batch_device_async)
@@ -684,7 +689,12 @@ struct HostMap {
   xe_map_def def{};
   uint32_t dkind = XE_DM_NONE;
   uint32_t cap = 0, kwords = 0;
-  uint32_t big = 0;  // HASH / LRU_HASH past the 23-bit handle slot field: 1 + its big-map number (XE_H_BIG)
+  uint32_t big = 0;  // HASH / LRU_HASH past the 23-bit handle slot field: 1 + its first big-map field (XE_H_BIG)
+  uint32_t big_nf = 0;  // ... and the number of fields it holds
+  // LRU_HASH: the most value ids the pool may have (value handles: 2^23 for a map that is not big, its
+  // fields' slots for a big one). Ids are not reused by the in-order replay, so a pool that would pass it
+  // is rebuilt compacted from the host mirror instead (ordered_upload)
+  uint64_t pool_limit = 1ull << XE_H_SLOT_BITS;
   uint64_t vals_bytes = 0, vals_alloc = 0;
   std::vector<uint8_t> vals;
   std::vector<uint64_t> keys;
@@ -1083,9 +1093,12 @@ uint32_t choose_nrep(uint64_t live, uint64_t vals_alloc, bool hash) {
 // vals += the replicas (replicas := 0); a HASH map only over the slots that hold or held an entry
 int fold_map(HostMap& m, xe_stream_t s) {
   const bool hash = m.dkind == XE_DM_HASH && m.def.value_size > 0;
-  const uint64_t words = m.dkind == XE_DM_LRU ? (uint64_t(m.pool_cap) * m.def.value_size + 7) / 8 : m.vals_alloc / 8;
+  const bool lru = m.dkind == XE_DM_LRU;
+  const uint64_t words = lru ? (uint64_t(m.pool_cap) * m.def.value_size + 7) / 8 : m.vals_alloc / 8;
+  // an LRU pool is folded only over the value ids handed out so far (its header word 3, on the device)
   return launch_rep_fold(m.d_vals, m.d_rep, m.rep_stride / 8, m.nrep, words, hash ? m.d_keys : nullptr,
-                         hash ? xe_hash_rwords(m.kwords) : 0, hash ? m.def.value_size : 8, m.cap, s);
+                         hash ? xe_hash_rwords(m.kwords) : 0, hash || lru ? m.def.value_size : 8, m.cap,
+                         lru ? (const void*)m.d_hdr : nullptr, s);
 }
 
 int map_alloc_device(HostMap& m) {
@@ -1365,7 +1378,14 @@ int ordered_upload(xe_vm* vm, HostMap& m, uint64_t slack, uint64_t slack_bytes) 
     // download / upload of the map and a second SPEC pass: ~50 ms of a 4M-packet C3-LRU batch).
     uint64_t room = 0;
     if (m.dkind == XE_DM_LRU) room = std::min<uint64_t>(m.def.max_entries, (256ull << 20) / std::max<uint32_t>(vs, 1));
-    const uint64_t pool = std::max(n, room) + slack;
+    uint64_t pool = std::max(n, room) + slack;
+    // an LRU pool never passes the value ids its handles can name (HostMap::pool_limit): this upload is
+    // compacted (the mirror's values get ids 0..n-1), and a batch that still runs out fails as one
+    // that outgrows the device (xe_interp.h lru_insert XE_EV_CAP) instead of aliasing another map's values
+    if (m.dkind == XE_DM_LRU) {
+      if (n + 1 > m.pool_limit) return -1;
+      pool = std::min(pool, m.pool_limit);
+    }
     std::vector<uint8_t> vals(std::max<uint64_t>(pool * vs, 8), 0);
     std::vector<uint32_t> elen(pool, 0);
     for (uint64_t i = 0; i < n; i++) {
@@ -1739,8 +1759,8 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
     case XE_MAP_HASH: case XE_MAP_PERCPU_HASH: case XE_MAP_HASH_OF_MAPS:
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_HASH;
-      m.cap = hash_cap(def->max_entries);
-      if (m.cap + 1 > (1u << (XE_H_SLOT_BITS + 3))) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 32M)");
+      if (def->max_entries > kHashCapMax) return fail(vm, XE_ERR_UNSUPPORTED, "hash map max_entries too large (<= 2^27)");
+      m.cap = uint32_t(hash_cap(def->max_entries));
       m.kwords = (def->key_size + 7) / 8;
       m.vals_bytes = uint64_t(m.cap + 1) * def->value_size;
       m.keys.assign(size_t(m.cap + 1) * m.kwords, 0);
@@ -1749,9 +1769,11 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
     case XE_MAP_LRU_HASH: case XE_MAP_LRU_PERCPU_HASH:
       if (def->key_size > XE_MAX_KEY) return fail(vm, XE_ERR_UNSUPPORTED, "device hash maps support keys up to 64 bytes");
       m.dkind = XE_DM_LRU;
-      m.cap = hash_cap(def->max_entries);
-      if (m.cap + 1 > (1u << (XE_H_SLOT_BITS + 3)) || def->max_entries >= (1u << (XE_H_SLOT_BITS + 2)))
-        return fail(vm, XE_ERR_UNSUPPORTED, "LRU hash map max_entries too large (< 32M)");
+      if (def->max_entries > (kHashCapMax >> 1)) return fail(vm, XE_ERR_UNSUPPORTED, "LRU hash map max_entries too large (<= 2^26)");
+      m.cap = uint32_t(hash_cap(def->max_entries));
+      // value ids: room for MaxEntries live values and as many inserts again before the pool is compacted
+      if (def->max_entries >= (1u << (XE_H_SLOT_BITS - 2)))
+        m.pool_limit = std::min<uint64_t>(kHashCapMax, uint64_t(big_fields(2ull * def->max_entries + (1u << 20))) << XE_H_SLOT_BITS);
       m.kwords = (def->key_size + 7) / 8;
       break;
     case XE_MAP_QUEUE: case XE_MAP_STACK:
@@ -1767,14 +1789,19 @@ int xe_add_map(xe_vm* vm, const xe_map_def* def, const void* init, size_t init_l
   {
     // value handles of slots / value ids past 23 bits (an LRU map's pool grows past MaxEntries) take the
     // big-map encoding, which needs map indices below XE_H_BIG (xe_internal.h)
-    uint32_t nbig = 0;
-    for (size_t i = 1; i < vm->maps.size(); i++) nbig += vm->maps[i].big ? 1 : 0;
-    const bool big = (m.dkind == XE_DM_HASH && m.cap + 1 > (1u << XE_H_SLOT_BITS)) ||
-                     (m.dkind == XE_DM_LRU && (m.cap + 1 > (1u << XE_H_SLOT_BITS) || def->max_entries >= (1u << (XE_H_SLOT_BITS - 2))));
-    if (big) {
-      if (nbig >= XE_H_BIG_MAPS) return fail(vm, XE_ERR_UNSUPPORTED, "at most 4 hash maps above 4M entries");
+    uint32_t nbig = 0, used = 0;
+    for (size_t i = 1; i < vm->maps.size(); i++) {
+      nbig += vm->maps[i].big ? 1 : 0;
+      used += vm->maps[i].big_nf;
+    }
+    const uint32_t nf = m.dkind == XE_DM_HASH ? big_fields(uint64_t(m.cap) + 1)
+                        : m.dkind == XE_DM_LRU ? big_fields(m.pool_limit) : 0;
+    if (nf > 1) {
+      if (used + nf > XE_H_BIG_FIELDS)
+        return fail(vm, XE_ERR_UNSUPPORTED, "the VM's hash maps above 4M entries need more than 2^28 value handles together");
       if (vm->maps.size() > XE_H_BIG - 1) return fail(vm, XE_ERR_UNSUPPORTED, "a hash map above 4M entries must be among the first 31 maps");
-      m.big = nbig + 1;
+      m.big = used + 1;
+      m.big_nf = nf;
     } else if (nbig && vm->maps.size() > XE_H_BIG - 1) {
       return fail(vm, XE_ERR_UNSUPPORTED, "at most 31 maps in a VM with a hash map above 4M entries");
     }
@@ -2357,7 +2384,10 @@ XeParams batch_params(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_
   P.n = n;
   P.nmaps = uint32_t(vm->maps.size() - 1);
   for (size_t i = 1; i < vm->maps.size(); i++)
-    if (vm->maps[i].big) P.bigmap[vm->maps[i].big - 1] = uint8_t(i);
+    for (uint32_t f = 0; vm->maps[i].big && f < vm->maps[i].big_nf; f++) {
+      P.bigmap[vm->maps[i].big - 1 + f] = uint8_t(i);
+      P.bigoff[vm->maps[i].big - 1 + f] = uint8_t(f);
+    }
   P.results = (xe_result*)d_results;
   P.verdicts = (uint32_t*)d_verdicts;
   P.regs = (xe_regs*)d_regs;
@@ -2739,7 +2769,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (size_t i = 1; i < vm->maps.size(); i++) {
       HostMap& m = vm->maps[i];
       if (m.nrep > 1 && fold_map(m, s)) return -1;
-      if (m.dkind == XE_DM_LRU && m.trep_r > 1 && launch_lru_tag_fold(m.d_tag, m.d_trep, m.pool_cap, m.trep_r, s)) return -1;
+      if (m.dkind == XE_DM_LRU && m.trep_r > 1 && launch_lru_tag_fold(m.d_tag, m.d_trep, m.pool_cap, m.trep_r, m.d_hdr, s)) return -1;
     }
     return 0;
   };
@@ -3100,6 +3130,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
                 launch_keyed_scan(&S, n, vm->d_ksort, &sb, s))
               return fail(vm, XE_ERR_DEVICE, "pop ranks");
             P.pop_mode = 2;
+            P.pop_map = pop_map;
             P.popbase = vm->d_popbase;
             if (int rc = pass()) return rc;
           }
@@ -3925,6 +3956,19 @@ int xe_debug_set_lru_epoch(xe_vm* vm, uint64_t epoch) {
   if (!vm || epoch > kLruEpochMax) return XE_ERR_INVAL;
   if (int rc = xe_sync(vm)) return rc;
   vm->lru_epoch = epoch;
+  return XE_OK;
+}
+
+int xe_debug_map_pool(xe_vm* vm, int32_t mi, uint64_t* room, uint64_t* next_id) {
+  HostMap* m = get_map(vm, mi);
+  if (!m || !m->ordered()) return XE_ERR_INVAL;
+  if (int rc = xe_sync(vm)) return rc;
+  set_device(vm->settings.device);
+  if (int rc = prepare_run(vm, vm->stream)) return rc;  // the device copy exists (it is built lazily)
+  uint64_t hdr[8];
+  if (d2h(hdr, m->d_hdr, 64, vm->stream) || dsync(vm->stream)) return fail(vm, XE_ERR_DEVICE, "map header");
+  if (room) *room = m->pool_cap;
+  if (next_id) *next_id = m->dkind == XE_DM_PERF ? hdr[0] : hdr[m->dkind == XE_DM_LRU ? 3 : 2];
   return XE_OK;
 }
 

@@ -337,6 +337,12 @@ class VM:
         """xe_debug_set_lru_epoch: the run counter of the LRU stamps (tests reach its renumbering)."""
         self._check(self.lib.debug_set_lru_epoch(self.h, epoch), "set LRU epoch")
 
+    def map_pool(self, m: int) -> tuple[int, int]:
+        """xe_debug_map_pool: (room, next fresh id) of an ordered map's device value pool."""
+        room, nxt = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.debug_map_pool(self.h, m, C.byref(room), C.byref(nxt)), "map pool")
+        return room.value, nxt.value
+
     def sync(self) -> None:
         """Complete every pipelined batch (in-order replays included)."""
         rc = self.lib.sync(self.h)

@@ -368,6 +368,10 @@ int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len)
 int xe_compile_kernel_source(const char* src, const char* arch, const char* dir, char* err, size_t errlen);
 /* the file name (in the cache directory) of the code object a source compiles to for `arch` */
 int xe_kernel_object_name(const char* src, const char* arch, char* buf, size_t cap);
+/* Kernel build statistics of this process: code objects loaded from the cache directory, per-program
+ * kernels compiled in-process by hiprtc (cache misses) and their total wall seconds. Diagnostics only
+ * (the -m gpu suite reports tests that compiled). */
+int xe_kernel_cache_stats(uint64_t* hits, uint64_t* compiles, double* compile_s);
 
 /* --- Step / VM.String (emulator/vm.go:137-173, 248-270): per-packet instruction trace ---
  * xe_trace_config selects packets by their index in each batch (at most XE_TRACE_MAX_PACKETS; duplicates
@@ -420,6 +424,9 @@ int xe_debug_set_schedule(xe_vm* vm, uint32_t sched);
 /* Set the run counter the LRU stamps carry in their top 16 bits (xe_interp.h lru_stamp), so a test can
  * reach the renumbering the runtime does before it wraps (0 <= epoch <= 0xffff) without 65,535 runs. */
 int xe_debug_set_lru_epoch(xe_vm* vm, uint64_t epoch);
+/* An ordered map's device value pool: its room (value ids) and the next fresh id (LRU_HASH / QUEUE /
+ * STACK; PERF: event records). Tests check that a stream of evicting batches keeps the pool's size. */
+int xe_debug_map_pool(xe_vm* vm, int32_t map, uint64_t* room, uint64_t* next_id);
 
 /* build / device info */
 const char* xe_version(void);

@@ -74,3 +74,42 @@ def _kernel_cache(request):
     t = threading.Thread(target=fill, daemon=True)
     t.start()
     yield d
+
+
+# ---- kernel compiles inside GPU tests (xe_kernel_cache_stats): a test that builds a per-program kernel
+# itself instead of loading it from the ahead-of-time cache (gobpfld_amd/aot.py) is named with the
+# seconds it spent, in the terminal summary
+_COMPILES: list[tuple[str, int, float]] = []
+
+
+def _kernel_stats():
+    import ctypes as C
+    from gobpfld_amd import _native as N
+    lib = N._product
+    if lib is None or not lib.has("kernel_cache_stats"):
+        return None
+    h, c, s = C.c_uint64(), C.c_uint64(), C.c_double()
+    lib.kernel_cache_stats(C.byref(h), C.byref(c), C.byref(s))
+    return h.value, c.value, s.value
+
+
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_call(item):
+    before = _kernel_stats() if item.get_closest_marker("gpu") else None
+    yield
+    if before is None:
+        return
+    after = _kernel_stats()
+    if after and after[1] > before[1]:
+        _COMPILES.append((item.nodeid, after[1] - before[1], after[2] - before[2]))
+
+
+def pytest_terminal_summary(terminalreporter):
+    st = _kernel_stats()
+    if st is None:
+        return
+    tr = terminalreporter
+    tr.section("per-program kernels")
+    tr.write_line(f"loaded from the cache: {st[0]}; compiled in-process: {st[1]} ({st[2]:.1f} s)")
+    for nodeid, n, s in sorted(_COMPILES, key=lambda x: -x[2])[:20]:
+        tr.write_line(f"  {s:8.1f} s  {n:3d} kernel(s)  {nodeid}")

@@ -49,6 +49,26 @@ def gpu_cases():
         cases.append((prog, [R.STATS_MAP], None, Settings(engine=JIT)))
     import test_key_shadow as KS
     cases += KS.kernel_cases()
+    # LRU evictions (tests/test_lru_evict.py): the learning program on its preloaded maps, the IMM-value
+    # update program, and every 8th ordered-map fuzz program (tests/test_fuzz_ordered.py)
+    import test_lru_evict as LE
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, LE.MAX))
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, LE.MAX - 10))
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, 0))
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), 5000, 5000))
+    for mx, _, _, _ in LE.IMM_CASES.values():
+        cases.append(lambda vm, mx=mx: LE._vm_setup(vm, LE._program_imm(), mx, mx))
+    # hash maps above 4M entries (tests/test_large_map.py)
+    import test_large_map as LM
+    for size in ("3M", "16M", "32M", "128M"):
+        cases.append((LM.prog_learn_u16(), [(MapDef(MAP_HASH, 4, 8, LM.SIZES[size]), None)], LM._entries(), Settings(engine=JIT)))
+    cases.append((LM.prog_learn_u32(), [(MapDef(MAP_HASH, 4, 8, LM.LIVE_MAX), None)], None, Settings()))
+    from fuzz import gen_ordered_program
+    import test_fuzz_ordered as FO
+    for seed in FO.JIT_SEEDS:
+        prog, maps, entries, settings = gen_ordered_program(seed)
+        settings.engine = JIT
+        cases.append((prog, maps, entries, settings))
     return cases
 
 

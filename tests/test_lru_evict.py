@@ -48,14 +48,20 @@ def _batch(ops, keys):
     return pk.view(np.uint8).reshape(-1).copy(), descs
 
 
+def _vm_setup(vm, prog, max_entries, live):
+    """An LRU_HASH(4, 4, max_entries) holding keys 0..live-1 (key k updated k-th: key 0 is the oldest)
+    and `prog` as the entrypoint (tests/kernel_cases.py builds the same VMs' kernels ahead of time)."""
+    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 4, max_entries))
+    for k in range(live):
+        vm.map_update(m, int(k).to_bytes(4, "little"), int(1000 + k).to_bytes(4, "little"))
+    vm.set_entrypoint(vm.add_raw_program(prog))
+    return m
+
+
 def _vm(lib, live):
     from gobpfld_amd.emulator import VM
     vm = VM(Settings(), lib=lib)
-    m = vm.add_map(MapDef(MAP_LRU_HASH, 4, 4, MAX))
-    for k in range(live):  # key k updated k-th: key 0 is the oldest
-        vm.map_update(m, int(k).to_bytes(4, "little"), int(1000 + k).to_bytes(4, "little"))
-    vm.set_entrypoint(vm.add_raw_program(_program()))
-    return vm, m
+    return vm, _vm_setup(vm, _program(), MAX, live)
 
 
 def _learning_batch(n, seed, touch_oldest=False, live=MAX):
@@ -182,3 +188,105 @@ def test_lru_order_log_churn_hostsim(hostsim_lib, oracle_lib):
 @pytest.mark.gpu
 def test_lru_order_log_churn_device(gpu_lib, oracle_lib):
     _check(_churn_case(gpu_lib), _churn_case(oracle_lib), [MODE_SEQUENTIAL] * 3)
+
+
+def _program_imm():
+    """As _program, plus op 2: an update whose value register is an IMM (r3 = 0). The reference
+    (maps_hash_lru.go:113-119, then :134-137) evicts the UsageList's tail of a full map for a new key
+    first and only then returns errMapValNoPtr (R0 = -14): the map shrinks by one."""
+    from gobpfld_amd.asm import JEQ, Asm
+    a = Asm()
+    a.ldx(4, 6, 1, 0)
+    a.ldx(4, 7, 6, 0)
+    a.ldx(4, 1, 6, 4).stx(4, 10, -4, 1)
+    a.st(4, 10, -8, 7)
+    a.ld_map(1, 1).mov64(2, src=10).add64(2, -4)
+    a.jmp(JEQ, 7, "lookup", imm=0)
+    a.jmp(JEQ, 7, "immval", imm=2)
+    a.mov64(3, src=10).add64(3, -8).mov64(4, 0).call(2).exit()
+    a.label("immval").mov64(3, 0).mov64(4, 0).call(2).exit()
+    a.label("lookup").call(1)
+    a.jmp(JEQ, 0, "miss", imm=0)
+    a.ldx(4, 0, 0, 0).exit()
+    a.label("miss").mov64(0, 0xFFFF).exit()
+    return a.assemble()
+
+
+def _imm_case(lib, max_entries, n, seed, mix=False, settings=None):
+    """A full LRU map (max_entries live keys), a batch of lookups of existing keys and one update of a new
+    key with an IMM value register; with mix, some pointer-valued updates of live keys as well."""
+    from gobpfld_amd.emulator import VM
+    vm = VM(settings or Settings(), lib=lib)
+    m = _vm_setup(vm, _program_imm(), max_entries, max_entries)
+    rng = np.random.default_rng(seed)
+    ops = np.zeros(n, dtype=np.uint32)
+    keys = rng.integers(max_entries // 2, max_entries, size=n).astype(np.uint32)
+    if mix:
+        upd = rng.random(n) < 0.2
+        ops[upd] = 1
+    ops[n // 3], keys[n // 3] = 2, 5000 + seed
+    out = []
+    for _ in range(2):  # a second batch on the same VM sees the first's final map
+        r = vm.run_batch(*_batch(ops, keys))
+        k, v = vm.map_dump(m)
+        out.append((r.results.copy(), r.stats["mode_used"], vm.map_lru_order(m), bytes(np.asarray(k)), bytes(np.asarray(v))))
+    count = vm.map_count(m)
+    vm.close()
+    return out, count
+
+
+IMM_CASES = {"full8": (8, 64, 1, False), "full64": (64, 400, 2, False), "full64_mixed": (64, 400, 3, True)}
+
+
+@pytest.mark.parametrize("case", sorted(IMM_CASES))
+def test_lru_imm_value_update_evicts_hostsim(hostsim_lib, oracle_lib, case):
+    mx, n, seed, mix = IMM_CASES[case]
+    (got, gc), (want, wc) = _imm_case(hostsim_lib, mx, n, seed, mix), _imm_case(oracle_lib, mx, n, seed, mix)
+    assert wc == mx - 1  # the first batch evicts one value and inserts none; the second finds room
+    _check(got, want, [None, None])
+    assert gc == wc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(IMM_CASES))
+def test_lru_imm_value_update_evicts_device(gpu_lib, oracle_lib, case):
+    mx, n, seed, mix = IMM_CASES[case]
+    (got, gc), (want, wc) = _imm_case(gpu_lib, mx, n, seed, mix), _imm_case(oracle_lib, mx, n, seed, mix)
+    assert wc == mx - 1
+    _check(got, want, [None, None])
+    assert gc == wc
+
+
+def _reuse_case(lib, batches=3, n=20000):
+    """A full LRU_HASH(4, 4, 64) on the one-lane path and batches that each insert n new keys: every
+    insert evicts. The replay hands an evicted value id to a later packet's insert (xe_interp.h
+    lru_free_push / lru_free_pop), so the value pool keeps its size over the stream; before, every insert
+    took a fresh id and the pool grew (by rebuilds with 4x the room) towards the ids value handles can
+    name. Results, UsageList and entries equal the oracle's after every batch."""
+    from gobpfld_amd.emulator import VM
+    vm = VM(Settings(mode=MODE_SEQUENTIAL), lib=lib)
+    m = _vm_setup(vm, _program(), MAX, MAX)
+    out, sizes = [], []
+    for b in range(batches):
+        ops = np.ones(n, dtype=np.uint32)
+        keys = (100000 + b * n + np.arange(n)).astype(np.uint32)
+        keys[::7] = keys[::7] - 3  # some keys inserted again a few packets later (a fresh insert: evicted since)
+        r = vm.run_batch(*_batch(ops, keys))
+        k, v = vm.map_dump(m)
+        out.append((r.results.copy(), r.stats["mode_used"], vm.map_lru_order(m), bytes(np.asarray(k)), bytes(np.asarray(v))))
+        sizes.append(vm.map_pool(m) if lib.has("debug_map_pool") else None)
+    vm.close()
+    return out, sizes
+
+
+def test_lru_replay_reuses_evicted_ids_hostsim(hostsim_lib, oracle_lib):
+    (got, sizes), (want, _) = _reuse_case(hostsim_lib), _reuse_case(oracle_lib)
+    _check(got, want, [MODE_SEQUENTIAL] * 3)
+    assert len({r for r, _ in sizes}) == 1 and sizes[-1][1] < 2 * MAX + 16, sizes  # no growth, ids reused
+
+
+@pytest.mark.gpu
+def test_lru_replay_reuses_evicted_ids_device(gpu_lib, oracle_lib):
+    (got, sizes), (want, _) = _reuse_case(gpu_lib), _reuse_case(oracle_lib)
+    _check(got, want, [MODE_SEQUENTIAL] * 3)
+    assert len({r for r, _ in sizes}) == 1 and sizes[-1][1] < 2 * MAX + 16, sizes

@@ -65,7 +65,7 @@ def alg_bytes_per_packet(name: str, sizes: np.ndarray) -> np.ndarray:
 ALG_DESC = {"c1": "16 desc + 4 verdict (program reads no packet bytes)"}
 
 
-PROFILE_ROUNDS = ("r5", "r4", "r3")  # committed PMC passes, newest first (a newer round's file supersedes)
+PROFILE_ROUNDS = ("r6", "r5", "r4", "r3")  # committed PMC passes, newest first (a newer round's file supersedes)
 
 
 def _profile(name: str, kind: str, n: int) -> tuple[dict | None, str | None]:
@@ -524,7 +524,9 @@ def side_line(name: str, n: int, steps: int, rank: int, world: int, dev, stream,
       c5 = configs[4]: 33,554,432 x 64 B per GPU, per-flow HASH counters {pkts, bytes} (1M flows); the
            exchange is one RCCL all-reduce of the per-flow deltas;
       c4 = configs[3]: 16,777,216 x 1500 B per GPU, the ~200-insn JEQ/JGT ACL (the 1500 B half of the
-           metric); no map, so the exchange reconciles nothing."""
+           metric); no map, so the exchange reconciles nothing;
+      c3 = configs[2]: 16,777,216 IMIX packets per GPU, 5-tuple HASH -> flow id, XDP_REDIRECT, per-flow
+           hit counters (64K flows, Zipf); checked against the header-derived truth like the others."""
     import torch
     from gobpfld_amd import workloads as W
     from gobpfld_amd.emulator import VM, Settings
@@ -555,8 +557,10 @@ def side_line(name: str, n: int, steps: int, rank: int, world: int, dev, stream,
             "alg_bytes_per_launch": int(alg), "alg_bytes_per_packet": "16 desc + min(len,64) header + 4 verdict",
             **sq_issue(name, n, k_s)}
     if name == "c4":
+        # what the same kernel time would be in GB/s if every packet byte were read (the ACL reads bytes
+        # 12-42 only): a throughput equivalent for 1500 B packets, not a roofline fraction
         roof["full_packet_bytes_per_launch"] = int(full)
-        roof["full_packet_frac"] = round(full / k_s / 1e9 / HBM_PEAK_GBS, 5)
+        roof["full_packet_equivalent_gbs"] = round(full / k_s / 1e9, 1)
     return {"workload": WORKLOADS[name], "packets_per_gpu": n, "n_gpus": world, "steps": steps,
             "value": round(n * world * steps / elapsed / 1e6, 3), "unit": "Mpkt/s",
             "ms_per_step": round(elapsed / steps * 1e3, 4), "avg_kernel_ms": round(k_s * 1e3, 4),
@@ -587,6 +591,9 @@ def main() -> None:
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run self-check")
     ap.add_argument("--c5-packets", type=int, default=32 * 1024 * 1024, help="C5 side line: packets per GPU")
     ap.add_argument("--c5-steps", type=int, default=8)
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 (IMIX, 5-tuple HASH) side line (C2 only)")
+    ap.add_argument("--c3-packets", type=int, default=16 * 1024 * 1024, help="C3 side line: packets per GPU")
+    ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--sync", action="store_true", help="one synchronous xe_run_batch_device per step (no pipelining)")
     ap.add_argument("--keyed-packets", type=int, default=4 * 1024 * 1024,
                     help="C3-learn batch of the keyed ordered-execution line (C2 runs only)")
@@ -662,7 +669,9 @@ def main() -> None:
     if rank == 0 and not args.no_e2e:
         e2e = e2e_baseline(vm, umem, descs)
     del umem
-    c5 = c4 = None
+    c5 = c4 = c3 = None
+    if name == "c2" and not args.no_c3:
+        c3 = side_line("c3", args.c3_packets, args.c3_steps, rank, world, dev, stream, dist)
     if name == "c2" and not args.no_c5:
         c5 = side_line("c5", args.c5_packets, args.c5_steps, rank, world, dev, stream, dist)
     if name == "c2" and not args.no_c4:
@@ -726,6 +735,7 @@ def main() -> None:
             "comm": comm,
             "c5": c5,
             "c4": c4,
+            "c3": c3,
             "ordered": ordered,
         }
         print(json.dumps(out), flush=True)

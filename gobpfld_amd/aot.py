@@ -66,7 +66,8 @@ def sources(cases, lib: N.Lib | None = None, variants=(0, 1, 2)) -> list[str]:
 def bench_cases() -> list:
     """The VMs bench.py and smoke() set up (full-size maps: their geometry is part of the kernel)."""
     from . import workloads as W
-    return [(lambda vm, n=name: W.setup_vm(vm, n)) for name in ("c1", "c2", "c2rmw", "c3", "c3learn", "c3lru", "c4", "c5", "bpf2bpf")]
+    return [(lambda vm, n=name: W.setup_vm(vm, n))
+            for name in ("c1", "c2", "c2rmw", "c3", "c3learn", "c3lru", "c3lrufull", "c4", "c5", "bpf2bpf")]
 
 
 def test_sources() -> list[str]:
@@ -75,8 +76,9 @@ def test_sources() -> list[str]:
     tests = str(ROOT / "tests")
     if tests not in sys.path:
         sys.path.insert(0, tests)
-    from kernel_cases import gpu_cases, gpu_lean_cases
-    return sources(gpu_cases(), variants=(0, 1)) + sources(gpu_lean_cases(), variants=(2,))
+    from kernel_cases import gpu_cases, gpu_lean_cases, gpu_seq_cases
+    return (sources(gpu_cases(), variants=(0, 1)) + sources(gpu_lean_cases(), variants=(2,)) +
+            sources(gpu_seq_cases(), variants=(3,)))
 
 
 def build(srcs: list[str], cache_dir: str | os.PathLike = KERNEL_DIR, workers: int | None = None,
@@ -88,6 +90,11 @@ def build(srcs: list[str], cache_dir: str | os.PathLike = KERNEL_DIR, workers: i
     d.mkdir(parents=True, exist_ok=True)
     srcs = list(dict.fromkeys(srcs))
     errors = kcache.fill(srcs, d, workers=workers)
+    slow = sorted(kcache.last_times, key=lambda x: -x[0])[:5]
+    for t, src in slow:  # the kernels that dominate a cold build (what made them slow: their #defines)
+        if t > 60:
+            print(f"aot: {t:.0f} s  " + " ".join(l.split()[1] + "=" + (l.split() + ["", ""])[2]
+                                                  for l in src.splitlines()[:14] if l.startswith("#define")), file=sys.stderr)
     removed = 0
     if prune:
         keep = {kcache.code_object_name(s) for s in srcs}
@@ -100,7 +107,9 @@ def build(srcs: list[str], cache_dir: str | os.PathLike = KERNEL_DIR, workers: i
 
 def build_all(workers: int | None = None, tests: bool = True) -> dict:
     """The benchmark / smoke kernels, and with `tests` the -m gpu suite's (then stale objects are pruned)."""
-    return build(sources(bench_cases()) + (test_sources() if tests else []), KERNEL_DIR, workers=workers, prune=tests)
+    # (variant 3: the scalar one-lane replay of the ordered-path lines)
+    return build(sources(bench_cases(), variants=(0, 1, 2, 3)) + (test_sources() if tests else []), KERNEL_DIR,
+                 workers=workers, prune=tests)
 
 
 if __name__ == "__main__":

@@ -33,6 +33,15 @@
 #pragma once
 #include "xe_internal.h"
 
+// XE_UNIFORM: the scalar form of the one-lane replay (a per-program kernel variant, xe_jit.cpp
+// XE_JV_SEQ). Every lane of the one wave runs the same packet with the same state, so the lane state is
+// wave-uniform: loads are read back with readfirstlane and the arithmetic and branches that follow run
+// on the scalar unit (one SALU instruction per cycle and SCC branches instead of wave64 VALU at four
+// cycles and EXEC-masked regions); an atomic is issued by lane 0 alone and its result broadcast.
+#ifndef XE_UNIFORM
+#define XE_UNIFORM 0
+#endif
+
 #if defined(__HIPCC__)
 #define XE_DEV __device__ __forceinline__
 #define XE_WAVE 64
@@ -52,42 +61,67 @@ XE_DEV void xe_pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
 // address space (global_load / global_atomic, vmcnt-only waits).
 #define XE_GP(T) __attribute__((address_space(1))) T*
 #define XE_LP(T) __attribute__((address_space(3))) T*
-XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) {
-  return __hip_atomic_fetch_add((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// wave-uniform copies of a value every lane holds (XE_UNIFORM); identity otherwise
+XE_DEV uint32_t xe_uni32(uint32_t v) { return XE_UNIFORM ? uint32_t(__builtin_amdgcn_readfirstlane(int(v))) : v; }
+XE_DEV uint64_t xe_uni64(uint64_t v) {
+  if (!XE_UNIFORM) return v;
+  return uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))))) << 32);
 }
-XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) {
+// an atomic issued once per wave in XE_UNIFORM (by lane 0, its result broadcast), by every lane otherwise
+#define XE_ONCE(T, expr)                                  \
+  do {                                                    \
+    if (!XE_UNIFORM) return expr;                         \
+    T r_ = 0;                                             \
+    if (__lane_id() == 0) r_ = expr;                      \
+    return (T)(xe_uni64(uint64_t(r_)));                   \
+  } while (0)
+#define XE_ONCE_VOID(stmt)                                \
+  do {                                                    \
+    if (!XE_UNIFORM || __lane_id() == 0) stmt;            \
+  } while (0)
+XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) {
+  XE_ONCE(unsigned long long, __hip_atomic_fetch_add((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+XE_DEV unsigned int xe_atomic_cas32_(unsigned int* p, unsigned int c, unsigned int v) {
   __hip_atomic_compare_exchange_strong((XE_GP(unsigned int))p, &c, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
   return c;
 }
+XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) {
+  XE_ONCE(unsigned int, xe_atomic_cas32_(p, c, v));
+}
 XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) {
-  __hip_atomic_fetch_or((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE_VOID(__hip_atomic_fetch_or((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV void xe_atomic_or64(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_fetch_or((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE_VOID(__hip_atomic_fetch_or((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV void xe_atomic_max64(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_fetch_max((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE_VOID(__hip_atomic_fetch_max((XE_GP(unsigned long long))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV unsigned int xe_atomic_add32(unsigned int* p, unsigned int v) {
-  return __hip_atomic_fetch_add((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE(unsigned int, __hip_atomic_fetch_add((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV unsigned int xe_load_relaxed32(unsigned int* p) {
-  return __hip_atomic_load((XE_GP(unsigned int))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return xe_uni32(__hip_atomic_load((XE_GP(unsigned int))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
+XE_DEV unsigned long long xe_atomic_cas64_(unsigned long long* p, unsigned long long c, unsigned long long v) {
   __hip_atomic_compare_exchange_strong((XE_GP(unsigned long long))p, &c, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
   return c;
 }
+XE_DEV unsigned long long xe_atomic_cas64(unsigned long long* p, unsigned long long c, unsigned long long v) {
+  XE_ONCE(unsigned long long, xe_atomic_cas64_(p, c, v));
+}
 XE_DEV unsigned int xe_atomic_min32(unsigned int* p, unsigned int v) {
-  return __hip_atomic_fetch_min((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE(unsigned int, __hip_atomic_fetch_min((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV unsigned long long xe_load_relaxed64(unsigned long long* p) {
-  return __hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return xe_uni64(__hip_atomic_load((XE_GP(unsigned long long))p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV void xe_atomic_max32(unsigned int* p, unsigned int v) {
-  __hip_atomic_fetch_max((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  XE_ONCE_VOID(__hip_atomic_fetch_max((XE_GP(unsigned int))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 XE_DEV uint64_t xe_lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
 XE_DEV uint32_t xe_shfl32(uint32_t v, int l) { return uint32_t(__shfl(int(v), l)); }
@@ -106,6 +140,8 @@ XE_DEV int xe_readlane(int v, int) { return v; }
 XE_DEV uint64_t xe_readlane64(uint64_t v, int) { return v; }
 XE_DEV int xe_lane() { return 0; }
 XE_DEV void xe_pin(uint64_t&) {}
+XE_DEV uint32_t xe_uni32(uint32_t v) { return v; }
+XE_DEV uint64_t xe_uni64(uint64_t v) { return v; }
 XE_DEV unsigned long long xe_atomic_add64(unsigned long long* p, unsigned long long v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 XE_DEV unsigned int xe_atomic_cas32(unsigned int* p, unsigned int c, unsigned int v) { __atomic_compare_exchange_n(p, &c, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); return c; }
 XE_DEV void xe_atomic_or32(unsigned int* p, unsigned int v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
@@ -1168,16 +1204,16 @@ XE_DEV uint64_t load_le(const uint8_t* p0, int size) {
   uintptr_t a = uintptr_t(p0);
   if ((a & uintptr_t(size - 1)) == 0) {
     switch (size) {
-      case 1: return *p;
-      case 2: return *(XE_GP(const uint16_t))p;
-      case 4: return *(XE_GP(const uint32_t))p;
-      default: return *(XE_GP(const uint64_t))p;
+      case 1: return xe_uni32(*p);
+      case 2: return xe_uni32(*(XE_GP(const uint16_t))p);
+      case 4: return xe_uni32(*(XE_GP(const uint32_t))p);
+      default: return xe_uni64(*(XE_GP(const uint64_t))p);
     }
   }
   uint64_t x = 0;
 #pragma unroll 1
   for (int b = 0; b < size; b++) x |= uint64_t(p[b]) << (8 * b);
-  return x;
+  return xe_uni64(x);
 }
 
 XE_DEV void store_le(uint8_t* p0, int size, uint64_t x) {
@@ -1201,7 +1237,9 @@ XE_DEV uint32_t hdr_dword(const XeLane& L, int pd) { return *(XE_LP(const uint32
 
 // little-endian read of `size` bytes at logical offset off (off + size <= hdr_len): the aligned
 // dwords covering the bytes and a funnel shift, no per-byte loop and no alignment branch
-XE_DEV uint64_t hdr_read(const XeLane& L, int off, int size) {
+XE_DEV uint64_t hdr_read_(const XeLane& L, int off, int size);
+XE_DEV uint64_t hdr_read(const XeLane& L, int off, int size) { return xe_uni64(hdr_read_(L, off, size)); }
+XE_DEV uint64_t hdr_read_(const XeLane& L, int off, int size) {
   const int pb = off + L.hsh;
   if (size == 1) return *hdr_at(L, pb);
   const int p0 = pb & ~3;
@@ -1659,7 +1697,7 @@ XE_DEV int ptr_read_range(XeLane& L, const XeParams& P, const XeReg& R, int64_t 
 }
 
 // ------------------------------------------------------------------ hash map
-XE_DEV uint64_t hash_word0(const XeDevMap& M, uint64_t slot) { return ((XE_GP(const uint64_t))M.keys)[slot * M.rwords]; }
+XE_DEV uint64_t hash_word0(const XeDevMap& M, uint64_t slot) { return xe_uni64(((XE_GP(const uint64_t))M.keys)[slot * M.rwords]); }
 XE_DEV uint32_t hash_state(const XeDevMap& M, uint64_t slot) { return uint32_t(hash_word0(M, slot)); }
 XE_DEV void hash_set_state(const XeDevMap& M, uint64_t slot, uint32_t st) {
   ((XE_GP(uint64_t))M.keys)[slot * M.rwords] = (hash_word0(M, slot) & ~0xffffffffull) | st;
@@ -1698,7 +1736,7 @@ XE_DEV void xe_group_load(XE_GP(const uint64_t) p, uint64_t* w) {
 #endif
 #pragma unroll
   for (int j = 0; j < XE_PROBE_GROUP / 8; j++)
-    w[j] = uint64_t(a[j >> 1][2 * (j & 1)]) | (uint64_t(a[j >> 1][2 * (j & 1) + 1]) << 32);
+    w[j] = xe_uni64(uint64_t(a[j >> 1][2 * (j & 1)]) | (uint64_t(a[j >> 1][2 * (j & 1) + 1]) << 32));
 }
 #endif
 XE_DEV int64_t hash_find(const XeDevMap& M, const uint64_t* kw, bool empty) {
@@ -3323,7 +3361,7 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body, Peek peek) {
       desc_fetch(P, c0 + lane, v, a, l);
       f = hdr_issue(P, L.hdrbuf, a, l, v);
       hdr_wait();
-#if XE_SEQ_PEEK
+#if XE_SEQ_PEEK && !XE_UNIFORM
       if (P.seq_prefetch & 2u) {
         lane_stage(L, P, v, a, l, f, L.hdrbuf, int(lane));
         L.peek = 1;
@@ -3334,7 +3372,8 @@ XE_DEV void seq_packets(XeLane& L, const XeParams& P, Body body, Peek peek) {
     }
 #pragma unroll 1
     for (uint32_t k = 0; k < m; k++) {
-      const bool valid = lane == 0;
+      // XE_UNIFORM: every lane runs packet k (the same state everywhere: the scalar replay)
+      const bool valid = XE_UNIFORM || lane == 0;
       // every lane stages packet k (only lane 0 runs it): the lane state is then wave-uniform, which
       // lets the compiler keep much of the replay's arithmetic on the scalar unit
       if (P.seq_prefetch)
@@ -3823,7 +3862,9 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
       P.regs[i] = g;
     }
   }
-  // batch statistics: per-lane step sums and wave-uniform status counts, flushed once per wave
+  // batch statistics: per-lane step sums and wave-uniform status counts, flushed once per wave (the
+  // scalar replay counts its packet once, on lane 0)
+  if (XE_UNIFORM) valid = valid && xe_lane() == 0;
   L.acc_steps += valid ? steps : 0;
 #if XE_HIST_FAST
   // status histogram: one ballot when every packet of the chunk ended OK (the common case)

@@ -893,6 +893,8 @@ struct xe_vm {
   void* kjit_fn = nullptr;
   void* ljit_fn = nullptr;   // the verdict-only variant (no result / register records)
   bool ljit_ready = false;
+  void* sjit_fn = nullptr;   // the scalar one-lane replay (xe_jit.cpp XE_JV_SEQ)
+  bool sjit_ready = false;
   bool kjit_ready = false;
   Timer t0, t1, t2;
   // room the ordered maps' device copies keep for one run (elements / events, event bytes), grown
@@ -939,7 +941,7 @@ struct xe_vm {
   uint8_t* d_skip = nullptr;
   uint32_t* d_ksmall = nullptr;  // XE_KS_WORDS counters (xe_internal.h layout)
   uint64_t keyed_n = 0;          // packets the per-packet arrays hold
-  uint32_t keyed_dcap = 0, keyed_kw = 0;
+  uint32_t keyed_dcap = 0, keyed_kw = 0;  // keyed_dcap: the D block's allocated capacity (K.dcap: in use)
   uint32_t keyed_dnext = 0;      // D table size for the next keyed batch (from the last one's D size)
   void* d_ksort = nullptr;
   size_t d_ksort_cap = 0;
@@ -1021,7 +1023,10 @@ static int keyed_alloc(xe_vm* vm, uint32_t n, uint32_t dcap) {
     K.counts = vm->d_ksmall + XE_KS_NO;
     K.cins = vm->d_ksmall + XE_KS_CINS;
   }
-  if (vm->keyed_dcap != dcap || vm->keyed_kw < kw) {
+  // the D block only grows: a stream that learns fewer keys per batch runs a smaller table inside the
+  // allocation it has (reallocating as the table shrank cost a synchronous free + alloc, ~1.8 ms, in
+  // the middle of the stream's second keyed batch)
+  if (vm->keyed_dcap < dcap || vm->keyed_kw < kw) {
     dev_free(K.dkey); dev_free(K.dkid); dev_free(K.dcomp); dev_free(K.cstart);
     dev_free(K.dfirst); dev_free(K.dvict); dev_free(K.ekey); dev_free(K.ekey2); dev_free(K.eval); dev_free(K.eval2);
     K.dkey = nullptr; K.dkid = nullptr; K.dcomp = K.cstart = nullptr;
@@ -2440,6 +2445,8 @@ int select_engine(xe_vm* vm, void*& jit, bool& jit_general) {
       vm->kjit_fn = nullptr;
       vm->ljit_ready = false;
       vm->ljit_fn = nullptr;
+      vm->sjit_ready = false;
+      vm->sjit_fn = nullptr;
     }
     jit = vm->jit_fn;
     jit_general = vm->jit_general;
@@ -2469,6 +2476,29 @@ void* keyed_kernel(xe_vm* vm, void* jit) {
   return vm->kjit_fn;
 #else
   (void)vm; (void)jit;
+  return nullptr;
+#endif
+}
+
+// The scalar replay variant of the selected per-program kernel (xe_jit.cpp XE_JV_SEQ, xe_interp.h
+// XE_UNIFORM) for in-order replays of at least kSeqScalarMin packets (a shorter replay costs less than
+// the variant's compile); null when the program has none (the general lane model).
+constexpr uint32_t kSeqScalarMin = 16384;
+void* seq_kernel(xe_vm* vm, void* jit) {
+#ifndef XE_HOSTSIM
+  if (!jit) return nullptr;
+  if (!vm->sjit_ready) {
+    const ProgTab t = prog_tab(vm);
+    bool cy = false, ge = false;
+    const char* jerr = "";
+    vm->sjit_fn = xe_jit_get(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry, vm->settings.device,
+                             vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), &cy, &ge, &jerr, 3, nullptr);
+    vm->sjit_ready = true;
+  }
+  return vm->sjit_fn;
+#else
+  (void)vm;
+  (void)jit;
   return nullptr;
 #endif
 }
@@ -2733,7 +2763,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         P.maps = vm->d_maps;
       }
       vm->t1.rec(s);
-      if (launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
+      // a long replay on the scalar variant of the per-program kernel (every lane runs the packet)
+      void* sj = (jit && !jit_general && n >= kSeqScalarMin) ? seq_kernel(vm, jit) : nullptr;
+      if (sj ? launch_jit(sj, &P, 1, 64, s) : launch(&P, 1, 64)) return fail(vm, XE_ERR_DEVICE, "kernel launch");
       vm->t2.rec(s);
       if (hostcalls && serve_hostcalls(vm->h_hostcall, s)) return fail(vm, XE_ERR_DEVICE, "kernel failed (host helpers)");
       if (read_aux()) return fail(vm, XE_ERR_DEVICE, "kernel failed");
@@ -3324,7 +3356,7 @@ int xe_prepare(xe_vm* vm) {
 // keyed variant, 2: its verdict-only variant), for a process that fills the kernel cache
 // (xe_compile_kernel_source).
 int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len) {
-  if (!vm || variant < 0 || variant > 2) return XE_ERR_INVAL;
+  if (!vm || variant < 0 || variant > 3) return XE_ERR_INVAL;
   // the host simulation generates the same sources (ahead-of-time kernel builds on a machine without a
   // GPU: gobpfld_amd/aot.py) but runs none of them
   if (int rc = xe_sync(vm)) return rc;
@@ -3336,6 +3368,7 @@ int xe_kernel_source(xe_vm* vm, int variant, char* buf, size_t cap, size_t* len)
   const size_t n = xe_jit_source_for(t.p.data(), t.n.data(), uint32_t(vm->programs.size() - 1), vm->entry,
                                      vm->dm_uploaded.data(), uint32_t(vm->dm_uploaded.size() - 1), variant, buf, cap);
   if (len) *len = n;
+  if (n == 0) return fail(vm, XE_ERR_UNSUPPORTED, "no such kernel variant for this program");
   return XE_OK;
 }
 
@@ -3347,6 +3380,12 @@ int xe_compile_kernel_source(const char*, const char*, const char*, char* err, s
   return XE_ERR_UNSUPPORTED;
 }
 int xe_kernel_object_name(const char*, const char*, char*, size_t) { return XE_ERR_UNSUPPORTED; }
+int xe_kernel_cache_stats(uint64_t* hits, uint64_t* compiles, double* compile_s) {
+  if (hits) *hits = 0;
+  if (compiles) *compiles = 0;
+  if (compile_s) *compile_s = 0;
+  return XE_OK;
+}
 #endif
 
 int xe_sync(xe_vm* vm) {

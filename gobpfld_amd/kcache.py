@@ -40,11 +40,13 @@ def _worker_init(lib_path: str) -> None:
     fn.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]
 
 
-def _worker_compile(job: tuple[str, str, str]) -> str:
+def _worker_compile(job: tuple[str, str, str]) -> tuple[str, float]:
+    import time
     src, arch, d = job
     err = C.create_string_buffer(4096)
+    t0 = time.perf_counter()
     rc = _worker_lib.xe_compile_kernel_source(src.encode(), arch.encode(), d.encode(), err, 4096)
-    return "" if rc == 0 else (err.value.decode(errors="replace") or "compile failed")
+    return ("" if rc == 0 else (err.value.decode(errors="replace") or "compile failed")), time.perf_counter() - t0
 
 
 def enable(lib, cache_dir: str | os.PathLike) -> str:
@@ -90,5 +92,10 @@ def fill(sources, cache_dir: str | os.PathLike, arch: str = "gfx950", workers: i
     n = min(workers or default_workers(), len(uniq))
     with ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context("spawn"), initializer=_worker_init,
                              initargs=(path,)) as ex:
-        errs = list(ex.map(_worker_compile, [(s, arch, d) for s in uniq]))
-    return [e for e in errs if e]
+        res = list(ex.map(_worker_compile, [(s, arch, d) for s in uniq]))
+    global last_times
+    last_times = [(t, s) for (_, t), s in zip(res, uniq)]
+    return [e for e, _ in res if e]
+
+
+last_times: list[tuple[float, str]] = []  # (seconds, source) of the last fill's compiles (cache hits ~0 s)

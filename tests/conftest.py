@@ -80,6 +80,7 @@ def _kernel_cache(request):
 # itself instead of loading it from the ahead-of-time cache (gobpfld_amd/aot.py) is named with the
 # seconds it spent, in the terminal summary
 _COMPILES: list[tuple[str, int, float]] = []
+_GPU_RAN = [False]
 
 
 def _kernel_stats():
@@ -96,6 +97,7 @@ def _kernel_stats():
 @pytest.hookimpl(hookwrapper=True)
 def pytest_runtest_call(item):
     before = _kernel_stats() if item.get_closest_marker("gpu") else None
+    _GPU_RAN[0] = _GPU_RAN[0] or before is not None
     yield
     if before is None:
         return
@@ -105,7 +107,7 @@ def pytest_runtest_call(item):
 
 
 def pytest_terminal_summary(terminalreporter):
-    st = _kernel_stats()
+    st = _kernel_stats() if _GPU_RAN[0] else None
     if st is None:
         return
     tr = terminalreporter

@@ -72,6 +72,22 @@ def gpu_cases():
     return cases
 
 
+def gpu_seq_cases():
+    """The cases whose in-order replays reach the scalar replay variant (>= 16,384 packets on the
+    per-program engine): its kernel (xe_jit.cpp XE_JV_SEQ)."""
+    import test_seq_scalar as SS
+    import test_lru_evict as LE
+    import test_ordered_par as O
+    cases = SS.cases()
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, LE.MAX))
+    cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, 0))
+    for build, mdef, entries, _ in O.CASES.values():
+        cases.append((build(), [mdef], entries, Settings()))
+    from gobpfld_amd import workloads as W
+    cases.append(lambda vm: W.setup_vm(vm, "c3lru"))
+    return cases
+
+
 def gpu_lean_cases():
     """The cases the suite also runs without result records (device-resident batches with verdicts only):
     their verdict-only kernel variant. The full-size config tests share bench.py's geometry (its kernels

@@ -74,13 +74,15 @@ def test_ordered_fuzz_device_interp(gpu_lib, oracle_lib):
         check_seed(gpu_lib, oracle_lib, seed, 128, ENGINE_INTERP)
 
 
-JIT_SEEDS = range(0, N_PROGRAMS, 8)
+# the per-program kernels of these programs take the dynamic block form over the general lane model with
+# every ordered-map helper compiled in: several CPU-minutes of hiprtc each, so the JIT leg keeps three
+# (built ahead of time: gobpfld_amd/aot.py via tests/kernel_cases.py); the interpreter leg runs all
+JIT_SEEDS = (0, 50, 125)
 
 
 @pytest.mark.gpu
 def test_ordered_fuzz_device_jit(gpu_lib, oracle_lib):
-    """Every 8th program on the per-program kernels (kernels built ahead of time: gobpfld_amd/aot.py via
-    tests/kernel_cases.py)."""
+    """Three of the programs on the per-program kernels (the same handlers, specialised per program)."""
     from gobpfld_amd.emulator import ENGINE_JIT
     for seed in JIT_SEEDS:
         check_seed(gpu_lib, oracle_lib, seed, 128, ENGINE_JIT)

@@ -40,8 +40,8 @@ def gpu_cases():
         cases.append(lambda vm, name=name, cap=cap: M._setup(vm, name, cap))
     cases.append(lambda vm: vm.set_entrypoint(vm.add_raw_program(G._program(G._map(vm)))))
     import test_ordered_par as O
-    for build, mdef, entries, _ in O.CASES.values():
-        cases.append((build(), [mdef], entries, Settings()))
+    for name, (build, _, entries, _) in O.CASES.items():
+        cases.append((build(), O.case_maps(name), entries, Settings()))
     from gobpfld_amd import workloads as W
     cases.append(lambda vm: W.setup_vm(vm, "c3lru"))
     import test_ref_examples as R
@@ -81,8 +81,8 @@ def gpu_seq_cases():
     cases = SS.cases()
     cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, LE.MAX))
     cases.append(lambda vm: LE._vm_setup(vm, LE._program(), LE.MAX, 0))
-    for build, mdef, entries, _ in O.CASES.values():
-        cases.append((build(), [mdef], entries, Settings()))
+    for name, (build, _, entries, _) in O.CASES.items():
+        cases.append((build(), O.case_maps(name), entries, Settings()))
     from gobpfld_amd import workloads as W
     cases.append(lambda vm: W.setup_vm(vm, "c3lru"))
     return cases

@@ -189,11 +189,15 @@ CASES = {
 }
 
 
+def case_maps(name):
+    """The maps a case runs with (its own, and the appends' QUEUE of lru_learn_queue)."""
+    return [CASES[name][1]] + ([QUEUE_BIG] if name == "lru_learn_queue" else [])
+
+
 def _run(lib, name, n, seed=11):
     build, mdef, entries, _ = CASES[name]
     umem, descs = packets(n, 64, seed=seed)
-    maps = [mdef] + ([QUEUE_BIG] if name == "lru_learn_queue" else [])
-    return run_one(lib, build(), maps, umem, descs, entries=entries)
+    return run_one(lib, build(), case_maps(name), umem, descs, entries=entries)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))

@@ -355,13 +355,20 @@ struct XeTailArgs {
 // List maps in a parallel run (XeParams::list): each QUEUE / STACK map's element count at the batch's
 // start, and per map the facts that decide afterwards whether the run equals packet order: sens = 1 + the
 // last packet whose list operation assumed no push happened before it in the batch, push = the first
-// packet that pushed (0xffffffff: none). Exact iff sens <= push for every map. popmask: maps popped.
+// packet that pushed (0xffffffff: none). Exact iff sens <= push for every map. popmask: maps popped;
+// newlist: a ranked pass met a pop of a list that has no rank slot yet (the pass is run again).
 struct XeListRun {
   uint32_t cnt0[64];
   uint32_t sens[64];
   uint32_t push[64];
   unsigned long long popmask;
-  unsigned long long pad;
+  unsigned long long newlist;
+};
+// Pops ranked in parallel: at most XE_POP_SLOTS popped lists per batch, a packet's pops of each counted in
+// 8 bits of one word (XeLane::npops, XeParams::popflag)
+#define XE_POP_SLOTS 4u
+struct XePopSlots {
+  uint8_t slot[64];
 };
 
 // per-launch parameters
@@ -417,11 +424,14 @@ struct XeParams {
   uint32_t trace_npk, trace_max;
   // QUEUE / STACK pops, peeks and lookups in a parallel run (xe_runtime.cpp, "list operations"): null
   // list: off (such an operation raises XE_FLAG_ORDERED). pop_mode 1 = the count pass (a lane stops at
-  // its packet's first list operation, flagging popflag[i] = 1 for a pop), 2 = the pass in which the
-  // packet's pop takes the element at its rank popbase[i] among the batch's pops in packet order.
+  // its packet's first list operation, flagging popflag[i] = 1 + the map it pops), 2 = a ranked pass: the
+  // k-th pop of list m by packet i takes the element at rank popbase[slot * pop_stride + i] + k among the
+  // batch's pops of m in packet order (slot = pop_slot[m]), and every packet writes the pops it made
+  // (8 bits per slot) to popflag[i]; the runtime reruns the pass until they are the counts it ranked by.
   XeListRun* list;
   uint32_t pop_mode;
-  uint32_t pop_map;       // pop_mode 2: the one list the batch pops (the ranks count its pops only)
+  uint32_t pop_stride;
+  uint8_t pop_slot[64];   // rank slot of each popped list (0xff: none)
   uint32_t* popflag;
   const uint32_t* popbase;
   // helper table (xe_set_helper): bit id of host[] = a host function, of nil[] = a nil entry

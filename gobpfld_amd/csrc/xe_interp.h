@@ -2097,10 +2097,11 @@ XE_DEV uint32_t list_at(const XeDevMap& M, uint64_t i) {  // Values[i] in Go sli
 // stack position: pushes land on top) assumes no push came before and records the packet in sens, and
 // the host replays the batch in order when a push did (push[m] < sens[m]).
 XE_DEV bool list_par(const XeParams& P) { return P.list && P.mode == XE_MODE_PARALLEL; }
-// (only the popped list loses elements: a peek or lookup of another list sees its start contents)
+// (only a popped list loses elements: a peek or lookup of another list sees its start contents)
 XE_DEV uint64_t list_pops_before(const XeLane& L, const XeParams& P, uint32_t m) {
-  if (P.pop_mode != 2 || m != P.pop_map) return 0;
-  return uint64_t(P.popbase[L.pidx]) + L.npops;
+  const uint32_t j = P.pop_mode == 2 ? uint32_t(P.pop_slot[m]) : 0xffu;
+  if (j >= XE_POP_SLOTS) return 0;
+  return uint64_t(P.popbase[uint64_t(j) * P.pop_stride + L.pidx]) + ((L.npops >> (8 * j)) & 0xffu);
 }
 XE_DEV void list_mark_sens(const XeLane& L, const XeParams& P, uint32_t m) { xe_atomic_max32(&P.list->sens[m], L.pidx + 1u); }
 // position (Go slice index) of Values[kv] for the lane's packet; false: out of range
@@ -2658,17 +2659,25 @@ XE_DEV int call_helper(XeLane& L, const XeParams& P, int64_t fn, uint32_t cm1 = 
       if (M.kind != XE_DM_LIST) return XE_E_MAP_OP | XE_E_IN_HELPER;  // "pop not available"
       XeReg val{0, 0, XE_KIND_IMM};
       if (xe_concurrent(P)) {
-        // the count pass flags the packet and stops it; the next pass pops the element at the packet's
-        // rank (one pop per packet: a second one replays the batch in order)
-        if (!list_par(P) || P.pop_mode == 0 || L.npops || (P.pop_mode == 2 && (!P.popflag[L.pidx] || m != P.pop_map))) return XE_EV_ORD;
+        // the count pass flags the packet's first pop and stops it; a ranked pass pops the element at
+        // the packet's rank among the batch's pops of the list, and counts the pop (the runtime checks
+        // the counts against the ones it ranked by, and runs the pass again until they agree)
+        if (!list_par(P) || P.pop_mode == 0) return XE_EV_ORD;
         if (P.pop_mode == 1) {
-          P.popflag[L.pidx] = 1u;
+          P.popflag[L.pidx] = 1u + m;
           xe_atomic_or64(&P.list->popmask, 1ull << m);
           return XE_EV_STOP;
         }
+        const uint32_t j = P.pop_slot[m];
+        if (j >= XE_POP_SLOTS) {  // a list nobody was ranked on: give it a slot and run the pass again
+          xe_atomic_or64(&P.list->popmask, 1ull << m);
+          xe_atomic_or64(&P.list->newlist, 1ull);
+          return XE_EV_STOP;
+        }
+        if (((L.npops >> (8 * j)) & 0xffu) == 0xffu) return XE_EV_ORD;  // (255 pops of one list in a packet)
         int64_t pos;
         if (list_pos(L, P, m, M, 0, pos)) val = XeReg{0, xe_h_make(XE_H_QVAL, m, list_at(M, uint64_t(pos))), XE_KIND_MEMPTR};
-        L.npops++;
+        L.npops += 1u << (8 * j);
       } else if (const uint64_t cnt = *map_hdr(M, 1)) {
         uint32_t id;
         if (*map_hdr(M, 4)) {
@@ -3810,6 +3819,9 @@ XE_DEV void lane_finish(XeLane& L, const XeParams& P, uint32_t i, bool valid, in
 #endif
   if (status == XE_ST_INTERNAL_ORDERED) xe_atomic_or32(P.flags, XE_FLAG_ORDERED);
   if (status == XE_ST_INTERNAL_CAPACITY) xe_atomic_or32(P.flags, XE_FLAG_CAPACITY);
+#if XE_HAS_ORDERED
+  if (P.pop_mode == 2 && valid) P.popflag[i] = L.npops;  // the pops the packet made, for the runtime's check
+#endif
 #if XE_KEYED
   if (P.mode == XE_MODE_SPEC) {  // the packet's key log
     if (valid) {

@@ -309,6 +309,25 @@ extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch,
   return hipcub::DeviceScan::ExclusiveSum(scratch, tmp, K->iota, K->ckey, int(n), s) == hipSuccess ? 0 : -1;
 }
 
+// Pops ranked in parallel (xe_runtime.cpp, list operations): mode 0 packs the count pass's flags (1 + the
+// map a packet pops first) into per-slot counts, mode 1 extracts slot `arg`'s 8-bit counts for its scan,
+// mode 2 sets *flag when a ranked pass's observed counts (src) differ from the ones ranked by (dst)
+__global__ void xe_pop_kernel(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t mode, uint32_t arg, XePopSlots sl,
+                              uint32_t* flag) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t v = src[i];
+    if (mode == 0) dst[i] = v ? 1u << (8u * (sl.slot[(v - 1u) & 63u] & 3u)) : 0u;
+    else if (mode == 1) dst[i] = (v >> (8u * arg)) & 0xffu;
+    else if (v != dst[i]) *flag = 1u;
+  }
+}
+extern "C" int xe_launch_pop(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t mode, uint32_t arg, XePopSlots sl,
+                             uint32_t* flag, hipStream_t s) {
+  const uint32_t blocks = n / 256 + 1 < 8192 ? n / 256 + 1 : 8192;
+  hipLaunchKernelGGL(xe_pop_kernel, dim3(blocks), dim3(256), 0, s, src, dst, n, mode, arg, sl, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // An LRU map's UsageList from its stamps (xe_runtime.cpp lru_relink): the pool's value ids sorted by
 // stamp, descending, then the first cnt of them linked in that order; `renumber` also rewrites the
 // stamps as their ranks from the tail (cnt .. 1: epoch 0, below every later run's stamps).

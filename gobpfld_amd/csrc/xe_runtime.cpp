@@ -50,6 +50,8 @@ extern "C" int xe_launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_b
 extern "C" int xe_launch_keyed_esort(const XeKeyed* K, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, hipStream_t s);
 extern "C" int xe_launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, hipStream_t s);
+extern "C" int xe_launch_pop(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t mode, uint32_t arg, XePopSlots sl,
+                             uint32_t* flag, hipStream_t s);
 extern "C" int xe_launch_lru_relink(uint64_t* tag, uint32_t pool, uint32_t cnt, uint32_t* link, uint64_t* hdr, void* scratch,
                                     size_t* bytes, int renumber, hipStream_t s);
 extern "C" int xe_launch_lru_tag_fold(uint64_t* tag, uint64_t* rep, uint32_t pool, uint32_t r, const uint64_t* hdr, hipStream_t s);
@@ -300,6 +302,16 @@ int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes
   for (uint32_t i = 0; i < n; i++) { K->ckey[i] = acc; acc += K->iota[i]; }
   return 0;
 }
+int launch_pop(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t mode, uint32_t arg, XePopSlots sl, uint32_t* flag,
+               xe_stream_t) {  // xe_kernel.hip xe_pop_kernel
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t v = src[i];
+    if (mode == 0) dst[i] = v ? 1u << (8u * (sl.slot[(v - 1u) & 63u] & 3u)) : 0u;
+    else if (mode == 1) dst[i] = (v >> (8u * arg)) & 0xffu;
+    else if (v != dst[i]) *flag = 1u;
+  }
+  return 0;
+}
 int launch_append(const XeAppendArgs* A, uint32_t, void* scratch, size_t* bytes, xe_stream_t) {
   if (!scratch) { *bytes = 8; return 0; }
   std::vector<std::pair<uint64_t, uint32_t>> v(A->k);
@@ -368,6 +380,10 @@ int launch_keyed_sort(const XeKeyed* K, uint32_t n, uint32_t end_bit, void* scra
 }
 int launch_append(const XeAppendArgs* A, uint32_t end_bit, void* scratch, size_t* bytes, xe_stream_t s) {
   return xe_launch_append(A, end_bit, scratch, bytes, s);
+}
+int launch_pop(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t mode, uint32_t arg, XePopSlots sl, uint32_t* flag,
+               xe_stream_t s) {
+  return xe_launch_pop(src, dst, n, mode, arg, sl, flag, s);
 }
 int launch_keyed_scan(const XeKeyed* K, uint32_t n, void* scratch, size_t* bytes, xe_stream_t s) {
   return xe_launch_keyed_scan(K, n, scratch, bytes, s);
@@ -954,7 +970,8 @@ struct xe_vm {
   // prefix sum (pop ranks)
   XeListRun* d_listrun = nullptr;
   uint32_t* d_popflag = nullptr;
-  uint32_t* d_popbase = nullptr;
+  uint32_t* d_popbase = nullptr;   // XE_POP_SLOTS x pop_n ranks
+  uint32_t* d_popused = nullptr;   // the per-slot pop counts the ranks were made from
   size_t pop_n = 0;
   // instruction trace (xe_trace_config): the traced packets (sorted), records kept per packet, device
   // copies (records, per-packet counts)
@@ -1711,7 +1728,7 @@ void xe_destroy(xe_vm* vm) {
   dev_free(vm->d_poison);
   stream_destroy(vm->cancel_stream);
   dev_free(vm->d_trace_pk); dev_free(vm->d_trace); dev_free(vm->d_trace_cnt);
-  dev_free(vm->d_listrun); dev_free(vm->d_popflag); dev_free(vm->d_popbase);
+  dev_free(vm->d_listrun); dev_free(vm->d_popflag); dev_free(vm->d_popbase); dev_free(vm->d_popused);
   host_free(vm->h_hostcall);
   for (auto& m : vm->maps) map_free_device(m);
   dev_free(vm->d_progs); dev_free(vm->d_prog_off); dev_free(vm->d_maps); dev_free(vm->d_aux);
@@ -3104,15 +3121,16 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     const bool lists = ordmaps && n > 0 && has_list_maps(vm);
     const bool pops = lists && may_pop(vm);
     bool list_conflict = false;
-    uint32_t pop_map = 0;
+    uint64_t popped = 0;  // the lists the batch's pops were ranked on (bit m)
     if (lists) {
       if (!vm->d_listrun && dev_alloc((void**)&vm->d_listrun, sizeof(XeListRun))) return fail(vm, XE_ERR_NOMEM, "device alloc (lists)");
       P.list = vm->d_listrun;
       if (pops && vm->pop_n < n) {
-        dev_free(vm->d_popflag); dev_free(vm->d_popbase);
-        vm->d_popflag = vm->d_popbase = nullptr;
+        dev_free(vm->d_popflag); dev_free(vm->d_popbase); dev_free(vm->d_popused);
+        vm->d_popflag = vm->d_popbase = vm->d_popused = nullptr;
         vm->pop_n = 0;
-        if (dev_alloc((void**)&vm->d_popflag, size_t(n) * 4) || dev_alloc((void**)&vm->d_popbase, size_t(n) * 4))
+        if (dev_alloc((void**)&vm->d_popflag, size_t(n) * 4) || dev_alloc((void**)&vm->d_popbase, size_t(n) * 4 * XE_POP_SLOTS) ||
+            dev_alloc((void**)&vm->d_popused, size_t(n) * 4))
           return fail(vm, XE_ERR_NOMEM, "device alloc (pop ranks)");
         vm->pop_n = n;
       }
@@ -3148,23 +3166,62 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         if (int rc = pass()) return rc;
         if (!conflict) {
           if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
-          if (lr.popmask & (lr.popmask - 1)) {  // pops from more than one list: one rank order per map is not kept
-            list_conflict = conflict = true;
-            flags |= XE_FLAG_ORDERED;
-          } else {
-            pop_map = lr.popmask ? uint32_t(__builtin_ctzll(lr.popmask)) : 0u;
-            XeKeyed S{};
-            S.iota = vm->d_popflag;
-            S.ckey = vm->d_popbase;
-            size_t sb = 0;
-            if (rollback(false) || ordered_hdr_restore(vm, ord_h0, s) || list_init() ||
-                launch_keyed_scan(&S, n, nullptr, &sb, s) || ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb) ||
-                launch_keyed_scan(&S, n, vm->d_ksort, &sb, s))
+          // Ranked passes: each popped list gets a slot; a packet's pops of it are counted in 8 bits of its
+          // word (the count pass's first pops, then what the last ranked pass observed), the counts of each
+          // slot are scanned into ranks, and the pass runs again from the batch's start until every packet
+          // made exactly the pops it was ranked by (a pop after a peek, a second pop, or pops from another
+          // list change what the count pass saw). Up to 4 passes; then, or with more than XE_POP_SLOTS
+          // popped lists, the batch replays in order.
+          uint64_t mask = lr.popmask;
+          bool ranked = false;
+          for (int it = 0; it < 4 && !conflict; it++) {
+            if (__builtin_popcountll(mask) > int(XE_POP_SLOTS)) break;
+            XePopSlots sl;
+            memset(sl.slot, 0xff, sizeof sl.slot);
+            uint32_t ns = 0;
+            for (uint32_t m = 0; m < 64; m++)
+              if ((mask >> m) & 1) sl.slot[m] = uint8_t(ns++);
+            memcpy(P.pop_slot, sl.slot, sizeof sl.slot);
+            P.pop_stride = n;
+            // the counts to rank by: packed count-pass flags first, then the last pass's observed counts
+            if (it == 0 ? launch_pop(vm->d_popflag, vm->d_popused, n, 0, 0, sl, nullptr, s)
+                        : d2d(vm->d_popused, vm->d_popflag, size_t(n) * 4, s))
               return fail(vm, XE_ERR_DEVICE, "pop ranks");
+            for (uint32_t j = 0; j < ns; j++) {
+              XeKeyed S{};
+              S.iota = vm->d_popflag;  // (free until the pass writes its observed counts)
+              S.ckey = vm->d_popbase + size_t(j) * n;
+              size_t sb = 0;
+              if (launch_pop(vm->d_popused, vm->d_popflag, n, 1, j, sl, nullptr, s) ||
+                  launch_keyed_scan(&S, n, nullptr, &sb, s) || ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, sb) ||
+                  launch_keyed_scan(&S, n, vm->d_ksort, &sb, s))
+                return fail(vm, XE_ERR_DEVICE, "pop ranks");
+            }
+            if (rollback(false) || ordered_hdr_restore(vm, ord_h0, s) || list_init()) return fail(vm, XE_ERR_DEVICE, "pop ranks");
             P.pop_mode = 2;
-            P.pop_map = pop_map;
             P.popbase = vm->d_popbase;
             if (int rc = pass()) return rc;
+            if (conflict) break;
+            if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
+            if (lr.newlist) {  // a pop of a list with no slot: rank it too
+              mask |= lr.popmask;
+              continue;
+            }
+            if (ensure_buf(&vm->d_ksort, &vm->d_ksort_cap, 256)) return fail(vm, XE_ERR_NOMEM, "pop ranks");
+            uint32_t* d_flag = (uint32_t*)vm->d_ksort;  // (the scans' scratch, free now)
+            uint32_t mismatch = 0;
+            if (dmemset(d_flag, 0, 4, s) || launch_pop(vm->d_popflag, vm->d_popused, n, 2, 0, sl, d_flag, s) ||
+                d2h(&mismatch, d_flag, 4, s) || dsync(s))
+              return fail(vm, XE_ERR_DEVICE, "pop ranks");
+            if (!mismatch) {
+              ranked = true;
+              popped = mask;
+              break;
+            }
+          }
+          if (!ranked && !conflict) {
+            list_conflict = conflict = true;
+            flags |= XE_FLAG_ORDERED;
           }
         }
       } else if (int rc = pass()) {
@@ -3237,17 +3294,25 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       // stack's pushes all came after its pops, so they land on the lowered top)
       if (ordmaps) {
         std::vector<uint64_t> h0 = ord_h0;
-        uint64_t k = 0;
-        if (pop_map) {
-          uint32_t last[2] = {0, 0};
-          if (d2h(&last[0], vm->d_popflag + (n - 1), 4, s) || d2h(&last[1], vm->d_popbase + (n - 1), 4, s) || dsync(s))
-            return fail(vm, XE_ERR_DEVICE, "pop count");
-          k = std::min<uint64_t>(uint64_t(last[0]) + last[1], ord_h0[pop_map * 8 + 1]);
-          if (vm->maps[pop_map].stack) h0[pop_map * 8 + 1] -= k;
+        std::vector<std::pair<uint32_t, uint64_t>> took;  // (list, its elements the batch popped)
+        if (popped) {
+          uint32_t last_used = 0;
+          if (d2h(&last_used, vm->d_popused + (n - 1), 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "pop count");
+          uint32_t j = 0;
+          for (uint32_t mi = 0; mi < 64; mi++) {
+            if (!((popped >> mi) & 1)) continue;
+            uint32_t base = 0;
+            if (d2h(&base, vm->d_popbase + size_t(j) * n + (n - 1), 4, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "pop count");
+            const uint64_t k = std::min<uint64_t>(uint64_t(base) + ((last_used >> (8 * j)) & 0xffu), ord_h0[mi * 8 + 1]);
+            if (vm->maps[mi].stack) h0[mi * 8 + 1] -= k;
+            if (k) took.push_back({mi, k});
+            j++;
+          }
         }
         if (ordered_finalize(vm, h0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
-        if (k) {
-          HostMap& m = vm->maps[pop_map];
+        for (const auto& t : took) {
+          HostMap& m = vm->maps[t.first];
+          const uint64_t k = t.second;
           uint64_t hdr[8];
           if (d2h(hdr, m.d_hdr, 64, s) || dsync(s)) return fail(vm, XE_ERR_DEVICE, "pops");
           if (!m.stack) hdr[0] = (hdr[0] + k) % m.list_cap;

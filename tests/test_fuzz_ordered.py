@@ -77,7 +77,7 @@ def test_ordered_fuzz_device_interp(gpu_lib, oracle_lib):
 # the per-program kernels of these programs take the dynamic block form over the general lane model with
 # every ordered-map helper compiled in: several CPU-minutes of hiprtc each, so the JIT leg keeps three
 # (built ahead of time: gobpfld_amd/aot.py via tests/kernel_cases.py); the interpreter leg runs all
-JIT_SEEDS = (0, 50, 125)
+JIT_SEEDS = (25, 75, 100)  # (programs without a keyed variant: the keyed ones compile for up to 20 min)
 
 
 @pytest.mark.gpu

@@ -129,6 +129,25 @@ def prog_consume(push=True, peek=None, two_pops=False):
     return a.assemble()
 
 
+def prog_two_lists():
+    """Pops from two lists in one batch (round 6: a rank slot per list): when packet[9] is even pop the
+    QUEUE (map 1), when packet[10] is even pop the STACK (map 2); the popped values (or 7 for an empty
+    list) go into R8 and the verdict."""
+    a = Asm()
+    _head(a, 16)
+    a.mov64(8, 7)
+    for m, byte, tag in ((1, 9, "q"), (2, 10, "s")):
+        a.ldx(1, 4, 6, byte).alu64(0x50, 4, 1).jmp(JNE, 4, "no" + tag, imm=0)
+        a.st(8, 10, -24, 0)
+        a.ld_map(1, m).mov64(2, src=10).add64(2, -24).call(88)
+        a.ldx(8, 3, 10, -24)
+        a.jmp(JEQ, 3, "no" + tag, imm=0)
+        a.ldx(8, 5, 3, 0).alu64(0x00, 8, src=5)
+        a.label("no" + tag)
+    a.label("out").mov64(0, src=8).alu64(0x50, 0, 3).exit()   # (_head jumps to "out" for a short packet)
+    return a.assemble()
+
+
 def prog_peek():
     """Reads only: peek at the front and look up element packet[1] % 64 by index (helper 1 on a queue);
     then push packet[0:8] — the reads sit inside the start contents, so the pushes do not move them."""
@@ -177,21 +196,27 @@ CASES = {
     "queue_consume": (prog_consume, LISTQ, LIST_PRELOAD, MODE_PARALLEL),
     "queue_consume_peek": (lambda: prog_consume(peek="after"), LISTQ, LIST_PRELOAD, MODE_PARALLEL),
     "stack_consume_peek": (lambda: prog_consume(peek="after", push=False), LISTS, LIST_PRELOAD, MODE_PARALLEL),
-    "queue_peek_then_pop": (lambda: prog_consume(peek="first"), LISTQ, LIST_PRELOAD, MODE_SEQUENTIAL),
+    # a peek before the pop: the count pass stops at the peek, the ranked pass finds the pop, and the pass
+    # runs again ranked by the pops it observed (round 6)
+    "queue_peek_then_pop": (lambda: prog_consume(peek="first"), LISTQ, LIST_PRELOAD, MODE_PARALLEL),
     "stack_consume": (lambda: prog_consume(push=False), LISTS, LIST_PRELOAD, MODE_PARALLEL),
     "queue_drained_no_push": (lambda: prog_consume(push=False), LISTQ, LIST_SHORT, MODE_PARALLEL),
+    # two pops in one packet: each packet's pops counted, ranked by the count (round 6)
+    "queue_two_pops": (lambda: prog_consume(two_pops=True), LISTQ, LIST_PRELOAD, MODE_PARALLEL),
     # ... and what must still replay in order: a pop past the start contents after an earlier push, a
-    # stack pop after a push, two pops in one packet
+    # stack pop after a push
     "queue_drained_push": (prog_consume, LISTQ, LIST_SHORT, MODE_SEQUENTIAL),
     "stack_consume_push": (prog_consume, LISTS, LIST_PRELOAD, MODE_SEQUENTIAL),
-    "queue_two_pops": (lambda: prog_consume(two_pops=True), LISTQ, LIST_PRELOAD, MODE_SEQUENTIAL),
     "queue_peek_only": (prog_peek, LISTQ, LIST_PRELOAD, MODE_PARALLEL),
+    # pops from a queue and a stack in one batch: one rank slot per list (round 6)
+    "two_lists_pop": (prog_two_lists, LISTQ, {0: LIST_PRELOAD[0], 1: LIST_PRELOAD[0]}, MODE_PARALLEL),
 }
 
 
 def case_maps(name):
     """The maps a case runs with (its own, and the appends' QUEUE of lru_learn_queue)."""
-    return [CASES[name][1]] + ([QUEUE_BIG] if name == "lru_learn_queue" else [])
+    extra = {"lru_learn_queue": [QUEUE_BIG], "two_lists_pop": [LISTS]}
+    return [CASES[name][1]] + extra.get(name, [])
 
 
 def _run(lib, name, n, seed=11):

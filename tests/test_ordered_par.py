@@ -247,7 +247,9 @@ def test_appends_hostsim_past_device_room(oracle_lib, hostsim_lib, name):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_appends_device_equal_oracle(gpu_lib, oracle_lib, name):
     # the list cases pop about every other packet: 4096 packets stay inside their 3072 preloaded elements
+    # (2048 where a popping packet pops twice; past the preloaded elements a batch replays in order)
     n = 4096 if name in ("queue_pop", "lru_update") or CASES[name][1] in (LISTQ, LISTS) else 262144
+    n = 2048 if name == "queue_two_pops" else n
     got = _run(gpu_lib, name, n)
     assert_same(got, _run(oracle_lib, name, n), name)
     assert got[0].stats["mode_used"] == CASES[name][3]

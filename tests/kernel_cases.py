@@ -102,4 +102,6 @@ def gpu_lean_cases():
     for name, _, cap, _ in M.CASES:
         cases.append(lambda vm, name=name, cap=cap: M._setup(vm, name, cap))
     cases.append(lambda vm: vm.set_entrypoint(vm.add_raw_program(G._program(G._map(vm)))))
+    import test_wave_steps as WS
+    cases.append(WS.setup_errors)
     return cases

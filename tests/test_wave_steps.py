@@ -1,11 +1,12 @@
-"""Step totals of the verdict-only kernel variant (xe_jit.cpp emit_body_blocks, wave step counts): a
-verdict-only batch reports no per-packet records, only the batch's step total (the instructions every
-packet retired, emulator/vm.go:117-173 counts each one up to and including the exit or the failing
-instruction), which the block form of a branchy program counts per wave on the scalar unit. These runs
-compare that total, the status histogram and the verdicts with the oracle's sequential VM: C4's ACL chain
-at the benchmark's geometry, and a program whose regions fail part-way (an unchecked packet read past the
-end of short packets: the lanes that leave a region early take back the steps they did not retire) and
-whose jump chain closes a region (counted per lane)."""
+"""Step totals of the verdict-only kernel variant (xe_jit.cpp XE_JV_LEAN, the block form of
+emit_body_blocks): a verdict-only batch reports no per-packet records, only the batch's step total (the
+instructions every packet retired, emulator/vm.go:117-173 counts each one up to and including the exit or
+the failing instruction) and its status histogram. These runs compare both, and the verdicts, with the
+oracle's sequential VM: C4's ACL chain at the benchmark's geometry, and a program whose regions fail
+part-way (an unchecked packet read past the end of short packets) and whose jump chain closes a region.
+(Round 6 measured counting these steps per wave on the scalar unit: C4 0.632 ms against 0.609 — the
+scalar unit issues at the same rate per SIMD as the vector one, and the counts cost more scalar
+instructions than the selects they replaced. Not kept.)"""
 import numpy as np
 import pytest
 

@@ -359,8 +359,9 @@ struct XeTailArgs {
 // newlist: a ranked pass met a pop of a list that has no rank slot yet (the pass is run again).
 struct XeListRun {
   uint32_t cnt0[64];
-  uint32_t sens[64];
-  uint32_t push[64];
+  uint32_t sens[64];    // 1 + the last packet with a position that assumed no earlier push (list_pos)
+  uint32_t push[64];    // the first packet that pushed
+  uint32_t senslo[64];  // the first packet with such a position (the runtime's segment cut)
   unsigned long long popmask;
   unsigned long long newlist;
 };

@@ -2103,7 +2103,10 @@ XE_DEV uint64_t list_pops_before(const XeLane& L, const XeParams& P, uint32_t m)
   if (j >= XE_POP_SLOTS) return 0;
   return uint64_t(P.popbase[uint64_t(j) * P.pop_stride + L.pidx]) + ((L.npops >> (8 * j)) & 0xffu);
 }
-XE_DEV void list_mark_sens(const XeLane& L, const XeParams& P, uint32_t m) { xe_atomic_max32(&P.list->sens[m], L.pidx + 1u); }
+XE_DEV void list_mark_sens(const XeLane& L, const XeParams& P, uint32_t m) {
+  xe_atomic_max32(&P.list->sens[m], L.pidx + 1u);
+  xe_atomic_min32(&P.list->senslo[m], L.pidx);
+}
 // position (Go slice index) of Values[kv] for the lane's packet; false: out of range
 XE_DEV bool list_pos(const XeLane& L, const XeParams& P, uint32_t m, const XeDevMap& M, int64_t kv, int64_t& pos) {
   const int64_t q = int64_t(list_pops_before(L, P, m)), cnt0 = int64_t(P.list->cnt0[m]);

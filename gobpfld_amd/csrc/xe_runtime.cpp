@@ -973,6 +973,7 @@ struct xe_vm {
   uint32_t* d_popbase = nullptr;   // XE_POP_SLOTS x pop_n ranks
   uint32_t* d_popused = nullptr;   // the per-slot pop counts the ranks were made from
   size_t pop_n = 0;
+  uint32_t seg_depth = 0;           // nesting of packet-order segments (xe_run_batch_device)
   // instruction trace (xe_trace_config): the traced packets (sorted), records kept per packet, device
   // copies (records, per-packet counts)
   std::vector<uint32_t> trace_pk;
@@ -2613,6 +2614,43 @@ void note_run(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t mo
 
 }  // namespace
 
+// Packet-order segments (XE_MODE_SEGMENTS): the batch's packets [0, cut) and [cut, n) as two batches, one
+// after the other (the second may be cut again), each through the whole path; their statistics summed.
+// The failed pass is rolled back first exactly as for the in-order fallback (map values, packets, the
+// ordered maps' headers, LRU stamps and values from their snapshots), and each segment takes a new LRU
+// epoch, so its stamps order after the segment before it as packet order does. Not with a packet trace
+// (it names packets by batch index), and at most kSegDepth cuts (the rest then takes the usual fallback).
+constexpr uint32_t kSegMin = 64, kSegDepth = 64;
+static bool segments_ok(const xe_vm* vm, const XeParams& P) { return !P.trace && vm->seg_depth < kSegDepth; }
+static int run_segments(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n, uint32_t cut,
+                        void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
+  xe_batch_stats a{}, b{};
+  auto at = [](void* p, size_t k) -> void* { return p ? (void*)((uint8_t*)p + k) : nullptr; };
+  vm->seg_depth++;
+  int rc = xe_run_batch_device(vm, d_umem, umem_len, d_desc, cut, d_results, d_verdicts, d_regs, stream, &a);
+  if (rc == XE_OK)
+    rc = xe_run_batch_device(vm, d_umem, umem_len, (const uint8_t*)d_desc + size_t(cut) * sizeof(xe_desc), n - cut,
+                             at(d_results, size_t(cut) * sizeof(xe_result)), at(d_verdicts, size_t(cut) * 4),
+                             at(d_regs, size_t(cut) * sizeof(xe_regs)), stream, &b);
+  vm->seg_depth--;
+  if (rc != XE_OK) return rc;
+  if (stats) {
+    stats->packets = n;
+    stats->steps = a.steps + b.steps;
+    for (int k = 0; k < 8; k++) stats->status_count[k] = a.status_count[k] + b.status_count[k];
+    // the slowest path any segment took; segments that all ran in parallel report XE_MODE_SEGMENTS
+    auto rank = [](uint32_t m) { return m == XE_MODE_SEQUENTIAL ? 3 : m == XE_MODE_KEYED ? 2 : 1; };
+    stats->mode_used = rank(a.mode_used) >= rank(b.mode_used) ? a.mode_used : b.mode_used;
+    if (stats->mode_used == XE_MODE_PARALLEL) stats->mode_used = XE_MODE_SEGMENTS;
+    stats->conflict = 1;
+    stats->kernel_ms = a.kernel_ms + b.kernel_ms;
+    stats->total_ms = a.total_ms + b.total_ms;
+    stats->engine_used = a.engine_used;
+    stats->grid_blocks = std::max(a.grid_blocks, b.grid_blocks);
+  }
+  return XE_OK;
+}
+
 int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
   if (!vm) return XE_ERR_INVAL;
@@ -3115,6 +3153,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     vm->last_grid = parallel_grid(vm, pj, general, n, P.nmaps);
     if (general && ensure_arena(vm, false, vm->last_grid * 256, P.gen)) return fail(vm, XE_ERR_NOMEM, "device alloc (arena)");
     uint32_t flags = 0;
+    uint32_t seg_cut = 0;  // > 0: the batch may run as packet-order segments cut there
     // QUEUE / STACK pops, peeks and lookups in parallel (xe_interp.h list_pos): the run's list record,
     // and for a program that may pop, a count pass first (which packets pop: their prefix sum is each
     // pop's rank in packet order), then the pass proper from the batch's start again
@@ -3140,7 +3179,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       memset(&lr, 0, sizeof lr);
       for (size_t i = 1; i < vm->maps.size() && i < 64; i++)
         if (vm->maps[i].dkind == XE_DM_LIST) lr.cnt0[i] = uint32_t(ord_h0[i * 8 + 1]);
-      for (int i = 0; i < 64; i++) lr.push[i] = 0xffffffffu;
+      for (int i = 0; i < 64; i++) lr.push[i] = lr.senslo[i] = 0xffffffffu;
       return h2d(vm->d_listrun, &lr, sizeof lr, s);
     };
     auto list_read = [&]() -> int { return d2h(&lr, vm->d_listrun, sizeof lr, s) || dsync(s); };
@@ -3233,6 +3272,15 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
           if (lr.sens[i] > lr.push[i]) list_conflict = true;
         if (list_conflict) {
           conflict = true;
+          // Segments: the packets before the first position that may have depended on an earlier push
+          // ran exactly; from there on the batch is a batch of its own whose start contents hold those
+          // pushes. The cut: per list, its first such packet (its first packet with a position, when that
+          // comes at or after its first push; else its first push, before which nothing was pushed).
+          if (!(flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY))) {
+            seg_cut = n;
+            for (int i = 0; i < 64; i++)
+              if (lr.sens[i] > lr.push[i]) seg_cut = std::min(seg_cut, lr.senslo[i] >= lr.push[i] ? lr.senslo[i] : lr.push[i]);
+          }
           flags |= XE_FLAG_ORDERED;
         }
       }
@@ -3248,6 +3296,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         }
       }
       break;
+    }
+    // (a segment costs a pass over what follows it: at least kSegMin packets, else the usual fallback)
+    if (conflict && mode == XE_MODE_AUTO && seg_cut >= kSegMin && seg_cut < n && segments_ok(vm, P)) {
+      if (rollback(false) || (ordmaps && ordered_hdr_restore(vm, ord_h0, s))) return fail(vm, XE_ERR_DEVICE, "rollback");
+      return run_segments(vm, d_umem, umem_len, d_desc, n, seg_cut, d_results, d_verdicts, d_regs, stream, stats);
     }
     if (conflict && (mode == XE_MODE_AUTO || (flags & XE_FLAG_CAPACITY))) {
       // order-dependent batch (or a lane out of arena): roll the maps back; map-entry writes take the

@@ -28,6 +28,7 @@ HASH_TYPES = (MAP_HASH, MAP_PERCPU_HASH, MAP_HASH_OF_MAPS, MAP_LRU_HASH, MAP_LRU
 LIST_TYPES = (MAP_QUEUE, MAP_STACK, MAP_PERF_EVENT_ARRAY)
 MODE_AUTO, MODE_PARALLEL, MODE_SEQUENTIAL, MODE_KEYED = 0, 1, 2, 3  # MODE_KEYED: mode_used only
 MODE_CANCELLED = 4  # mode_used of a pipelined batch VM.cancel dropped
+MODE_SEGMENTS = 5  # mode_used: packet-order segments, each in parallel (a list position after an earlier push)
 E_HOST_HELPER, E_IN_HELPER = 17, 0x80
 ENGINE_AUTO, ENGINE_INTERP, ENGINE_JIT = 0, 1, 2
 

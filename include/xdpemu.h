@@ -128,6 +128,9 @@ extern "C" {
 #define XE_MODE_SEQUENTIAL 2 /* exact packet order on one device lane                             */
 #define XE_MODE_KEYED 3      /* (xe_batch_stats.mode_used only) map-entry writes: per-key chains  */
 #define XE_MODE_CANCELLED 4  /* (xe_batch_stats.mode_used only) a pipelined batch xe_cancel dropped */
+#define XE_MODE_SEGMENTS 5   /* (xe_batch_stats.mode_used only) XE_MODE_AUTO ran the batch as packet-order */
+                             /* segments, each in parallel: a QUEUE / STACK position depended on a push of */
+                             /* an earlier packet, so the packets from there on ran after those before it */
 
 /* AF_XDP descriptor, exactly the layout of gobpfld's xsk.go:695-701 */
 typedef struct xe_desc {

@@ -42,6 +42,10 @@ def gpu_cases():
     import test_ordered_par as O
     for name, (build, _, entries, _) in O.CASES.items():
         cases.append((build(), O.case_maps(name), entries, Settings()))
+    import test_segments as SG
+    for name in SG.CASES:
+        prog, maps, entries = SG._case(name)
+        cases.append((prog, maps, entries, Settings()))
     from gobpfld_amd import workloads as W
     cases.append(lambda vm: W.setup_vm(vm, "c3lru"))
     import test_ref_examples as R

@@ -15,7 +15,7 @@ import pytest
 
 from gobpfld_amd.asm import JEQ, JGT, JNE, Asm
 from gobpfld_amd.emulator import (MAP_LRU_HASH, MAP_PERF_EVENT_ARRAY, MAP_QUEUE, MAP_STACK, MODE_KEYED, MODE_PARALLEL,
-                                  MODE_SEQUENTIAL, MapDef)
+                                  MODE_SEGMENTS, MODE_SEQUENTIAL, MapDef)
 from parity import assert_same, packets, run_one
 
 
@@ -186,7 +186,8 @@ CASES = {
     "queue": (prog_push, QUEUE, PRELOAD, MODE_PARALLEL),
     "stack": (prog_push, STACK, PRELOAD, MODE_PARALLEL),
     "perf": (prog_perf, PERF, None, MODE_PARALLEL),
-    "queue_pop": (lambda: prog_push(pop=True), QUEUE, PRELOAD, MODE_SEQUENTIAL),
+    # a rare pop that runs past the 3 preloaded elements after earlier pushes: packet-order segments
+    "queue_pop": (lambda: prog_push(pop=True), QUEUE, PRELOAD, MODE_SEGMENTS),
     "lru_lookup": (prog_lru, LRU, LRU_PRELOAD, MODE_PARALLEL),
     "lru_update": (lambda: prog_lru(update=True), LRU, LRU_PRELOAD, MODE_SEQUENTIAL),
     # LRU learning without eviction: the keyed path (misses insert, later packets of the key hit it)
@@ -203,9 +204,10 @@ CASES = {
     "queue_drained_no_push": (lambda: prog_consume(push=False), LISTQ, LIST_SHORT, MODE_PARALLEL),
     # two pops in one packet: each packet's pops counted, ranked by the count (round 6)
     "queue_two_pops": (lambda: prog_consume(two_pops=True), LISTQ, LIST_PRELOAD, MODE_PARALLEL),
-    # ... and what must still replay in order: a pop past the start contents after an earlier push, a
-    # stack pop after a push
-    "queue_drained_push": (prog_consume, LISTQ, LIST_SHORT, MODE_SEQUENTIAL),
+    # a pop past the start contents after earlier pushes: the packets before the first such pop run in
+    # parallel, the rest as a batch of its own that starts with their pushes (packet-order segments, round 6)
+    "queue_drained_push": (prog_consume, LISTQ, LIST_SHORT, MODE_SEGMENTS),
+    # ... and what must still replay in order: stack pops interleaved with pushes from the first packets on
     "stack_consume_push": (prog_consume, LISTS, LIST_PRELOAD, MODE_SEQUENTIAL),
     "queue_peek_only": (prog_peek, LISTQ, LIST_PRELOAD, MODE_PARALLEL),
     # pops from a queue and a stack in one batch: one rank slot per list (round 6)

@@ -3276,7 +3276,10 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
           // ran exactly; from there on the batch is a batch of its own whose start contents hold those
           // pushes. The cut: per list, its first such packet (its first packet with a position, when that
           // comes at or after its first push; else its first push, before which nothing was pushed).
-          if (!(flags & (XE_FLAG_ORDERED | XE_FLAG_CAPACITY))) {
+          // (Any cut keeps the packet loop's order — two batches are the same loop — so a pass that also
+          // ran out of an ordered map's room still cuts: each segment grows the room itself. A lane that
+          // needed an ordered map write elsewhere would need the fallback in every segment: no cut.)
+          if (!(flags & XE_FLAG_ORDERED)) {
             seg_cut = n;
             for (int i = 0; i < 64; i++)
               if (lr.sens[i] > lr.push[i]) seg_cut = std::min(seg_cut, lr.senslo[i] >= lr.push[i] ? lr.senslo[i] : lr.push[i]);
@@ -3285,8 +3288,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
         }
       }
       // appends past an ordered map's device room: the atomics counted every attempted append, so the
-      // room grows to what the batch needs and the parallel pass runs once more
-      if (ordmaps && attempt == 0 && (flags & XE_FLAG_CAPACITY) && !(flags & XE_FLAG_ORDERED)) {
+      // room grows to what the batch needs and the parallel pass runs once more (up to three times: a
+      // count pass stops its packets at their first pop, so its appends undercount the ranked pass's)
+      if (ordmaps && attempt < 3 && (flags & XE_FLAG_CAPACITY) && !(flags & XE_FLAG_ORDERED)) {
         const int g = ordered_grow(vm, ord_h0, s);
         if (g < 0) return fail(vm, XE_ERR_DEVICE, "ordered map room");
         if (g == 1) {

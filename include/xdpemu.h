@@ -183,7 +183,7 @@ typedef struct xe_batch_stats {
     uint64_t packets;
     uint64_t steps;            /* instructions retired over the batch */
     uint64_t status_count[8];  /* histogram of xe_result.status */
-    uint32_t mode_used;        /* XE_MODE_PARALLEL, XE_MODE_KEYED or XE_MODE_SEQUENTIAL */
+    uint32_t mode_used;        /* XE_MODE_PARALLEL, _KEYED, _SEQUENTIAL, _SEGMENTS (_CANCELLED) */
     uint32_t conflict;         /* 1 if the parallel run was order-dependent */
     float kernel_ms;           /* device time of the interpreter launch(es) */
     float total_ms;            /* device time of the whole call */

@@ -42,6 +42,9 @@ def gpu_cases():
     import test_ordered_par as O
     for name, (build, _, entries, _) in O.CASES.items():
         cases.append((build(), O.case_maps(name), entries, Settings()))
+    import test_rule_chain as RC
+    for kind in RC.KINDS:
+        cases.append((RC.prog_rules(kind), [], None, Settings(engine=JIT)))
     import test_segments as SG
     for name in SG.CASES:
         prog, maps, entries = SG._case(name)
@@ -108,4 +111,7 @@ def gpu_lean_cases():
     cases.append(lambda vm: vm.set_entrypoint(vm.add_raw_program(G._program(G._map(vm)))))
     import test_wave_steps as WS
     cases.append(WS.setup_errors)
+    import test_rule_chain as RC
+    for kind in RC.KINDS:
+        cases.append((RC.prog_rules(kind), [], None, Settings(engine=JIT)))
     return cases

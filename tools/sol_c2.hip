@@ -11,6 +11,8 @@
 // The best variant's time is the floor for the emulator kernel on this workload: what the access
 // pattern itself costs, the emulation removed.
 //   hipcc --offload-arch=gfx950 -O3 tools/sol_c2.hip -o tools/sol_c2 && tools/sol_c2
+// C4's shape (round 6): `tools/sol_c2 1500 3` — 1,500-B packets back to back, the three rows that hold
+// header bytes [12, 42) from the 16-B aligned address at or below byte 12 (the emulator's C4 window).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -36,10 +38,9 @@ __device__ __forceinline__ void glds16(GP(const uint8_t) src, uint32_t d) {
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_vm1() { asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); }
 
-constexpr int ROWS = 2;
 constexpr int ROWB = 64 * 16;  // one row for the wave
 
-template <int V>
+template <int V, int ROWS>
 __global__ void __launch_bounds__(256) sol(const uint8_t* __restrict__ umem, const Desc* __restrict__ desc, uint32_t n,
                                            uint32_t* __restrict__ ver) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][V == 2 ? 3 : 2][ROWS * ROWB];
@@ -51,7 +52,7 @@ __global__ void __launch_bounds__(256) sol(const uint8_t* __restrict__ umem, con
     a = (c < nchunks && i < n) ? ((GP(const uint64_t))(desc + i))[0] : 0;
   };
   auto issue = [&](uint64_t a, int buf) {
-    GP(const uint8_t) src = (GP(const uint8_t))(umem + a);
+    GP(const uint8_t) src = (GP(const uint8_t))(umem + ((a + 12) & ~uint64_t(15)));
     const uint32_t d = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(uintptr_t(&lds[w][buf][0])))));
     for (int k = 0; k < ROWS; k++) glds16(src + 16 * k, d + k * ROWB);
   };
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(256) sol(const uint8_t* __restrict__ umem, con
     u4 r0[ROWS], r1[ROWS];
     int cur = 0;
     if (V == 1) issue(a0, 0);
-    else for (int k = 0; k < ROWS; k++) r0[k] = *(GP(const u4))(umem + a0 + 16 * k);
+    else for (int k = 0; k < ROWS; k++) r0[k] = *(GP(const u4))(umem + ((a0 + 12) & ~uint64_t(15)) + 16 * k);
     for (;;) {
       wait_vm();
       if (V == 3) {
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(256) sol(const uint8_t* __restrict__ umem, con
       const uint32_t c1 = c + nwaves, c2 = c1 + nwaves;
       if (c1 < nchunks) {
         if (V == 1) issue(a1, cur ^ 1);
-        else for (int k = 0; k < ROWS; k++) r1[k] = *(GP(const u4))(umem + a1 + 16 * k);
+        else for (int k = 0; k < ROWS; k++) r1[k] = *(GP(const u4))(umem + ((a1 + 12) & ~uint64_t(15)) + 16 * k);
       }
       uint64_t a2;
       dload(c2, a2);
@@ -124,9 +125,12 @@ __global__ void __launch_bounds__(256) sol(const uint8_t* __restrict__ umem, con
 
 int main(int argc, char** argv) {
   const uint32_t n = 16u << 20;
-  const uint64_t bytes = uint64_t(n) * 64;
+  const uint32_t pkt = argc > 1 ? uint32_t(atoi(argv[1])) : 64u;
+  const int rows = argc > 2 ? atoi(argv[2]) : 2;
+  if (rows != 2 && rows != 3) return 2;
+  const uint64_t bytes = uint64_t(n) * pkt + 64;
   std::vector<Desc> hd(n);
-  for (uint32_t i = 0; i < n; i++) hd[i] = Desc{uint64_t(i) * 64, 64, 0};
+  for (uint32_t i = 0; i < n; i++) hd[i] = Desc{uint64_t(i) * pkt, pkt, 0};
   uint8_t* um;
   Desc* dd;
   uint32_t* ver;
@@ -141,10 +145,17 @@ int main(int argc, char** argv) {
     for (int bpc : {4, 6, 8}) {
       const uint32_t blocks = 256 * bpc;
       auto launch = [&]() {
-        if (V == 0) hipLaunchKernelGGL(sol<0>, dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
-        if (V == 1) hipLaunchKernelGGL(sol<1>, dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
-        if (V == 2) hipLaunchKernelGGL(sol<2>, dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
-        if (V == 3) hipLaunchKernelGGL(sol<3>, dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+        if (rows == 2) {
+          if (V == 0) hipLaunchKernelGGL((sol<0, 2>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 1) hipLaunchKernelGGL((sol<1, 2>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 2) hipLaunchKernelGGL((sol<2, 2>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 3) hipLaunchKernelGGL((sol<3, 2>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+        } else {
+          if (V == 0) hipLaunchKernelGGL((sol<0, 3>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 1) hipLaunchKernelGGL((sol<1, 3>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 2) hipLaunchKernelGGL((sol<2, 3>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+          if (V == 3) hipLaunchKernelGGL((sol<3, 3>), dim3(blocks), dim3(256), 0, 0, um, dd, n, ver);
+        }
       };
       float best = 1e9;
       for (int rep = 0; rep < 12; rep++) {  // one launch at a time (idle between launches)
@@ -163,8 +174,8 @@ int main(int argc, char** argv) {
       (void)hipEventSynchronize(e1);
       (void)hipEventElapsedTime(&b2b, e0, e1);
       b2b /= 20;
-      printf("{\"variant\": %d, \"blocks_per_cu\": %d, \"best_ms\": %.4f, \"b2b_ms\": %.4f, \"alg_TBps_best\": %.3f, "
-             "\"alg_TBps_b2b\": %.3f}\n", V, bpc, best, b2b, alg / (best * 1e-3) / 1e12, alg / (b2b * 1e-3) / 1e12);
+      printf("{\"pkt\": %u, \"rows\": %d, \"variant\": %d, \"blocks_per_cu\": %d, \"best_ms\": %.4f, \"b2b_ms\": %.4f, \"alg_TBps_best\": %.3f, "
+             "\"alg_TBps_b2b\": %.3f}\n", pkt, rows, V, bpc, best, b2b, alg / (best * 1e-3) / 1e12, alg / (b2b * 1e-3) / 1e12);
       fflush(stdout);
     }
   }

@@ -45,6 +45,8 @@ def gpu_cases():
     import test_rule_chain as RC
     for kind in RC.KINDS:
         cases.append((RC.prog_rules(kind), [], None, Settings(engine=JIT)))
+    for seed in RC.RANDOM_SEEDS:
+        cases.append((RC.prog_random(seed), [], None, Settings(engine=JIT)))
     import test_segments as SG
     for name in SG.CASES:
         prog, maps, entries = SG._case(name)

@@ -11,7 +11,7 @@ packets (every JNE taken), one and three further tests per rule."""
 import numpy as np
 import pytest
 
-from gobpfld_amd.asm import JEQ, JGT, JNE, JSGE, Asm
+from gobpfld_amd.asm import JEQ, JGE, JGT, JNE, JSGE, JSGT, JSLE, JSLT, Asm
 from gobpfld_amd.emulator import ENGINE_JIT, VM, Settings
 from parity import assert_same, run_one
 
@@ -132,3 +132,97 @@ def test_rule_chain_verdict_only_steps(gpu_lib, oracle_lib, kind):
     assert (d_ver.cpu().numpy().view(np.uint32) == ro.verdicts).all()
     assert st["steps"] == ro.stats["steps"]
     assert list(st["status_count"][:8]) == list(np.bincount(ro.results["status"], minlength=8)[:8])
+
+
+# ---- random rule chains: the dispatch's choices against the oracle's walk over many shapes
+# (the reference has no JSET / JLT / JLE instruction: emulator/ decodes them and stops, xe_runtime.cpp)
+EXTRA_OPS = [JNE, JEQ, JGT, JGE, JSGT, JSGE, JSLT, JSLE]
+FIELDS = {9: (8, 1), 5: (10, 2), 4: (16, 8), 3: (24, 4)}  # register: (packet offset, bytes)
+
+
+def random_rules(seed):
+    """(wide, extra-test shape [(register, op, wide)], rules [(key, [imm per extra test], verdict)])"""
+    rng = np.random.default_rng(1000 + seed)
+    wide = bool(rng.random() < 0.5)
+    shape = [(int(rng.choice(list(FIELDS))), int(rng.choice(EXTRA_OPS)), bool(rng.random() < 0.5))
+             for _ in range(int(rng.integers(0, 4)))]
+    pool = [int(x) for x in rng.integers(-2**31, 2**31, size=int(rng.integers(3, 20)))]
+    rules = []
+    lo = max(8, 33 // (1 + len(shape)) + 1)  # (the block form: more than 32 conditional jumps)
+    for _ in range(int(rng.integers(lo, max(lo, 40) + 1))):
+        key = int(rng.choice(pool))
+        imms = [int(rng.integers(-300, 70000)) if rng.random() < 0.8 else int(rng.integers(-2**31, 2**31))
+                for _ in shape]
+        rules.append((key, imms, int(rng.integers(1, 4))))
+    return wide, shape, rules
+
+
+def prog_random(seed):
+    wide, shape, rules = random_rules(seed)
+    a = Asm()
+    a.ldx(4, 6, 1, 0).ldx(4, 7, 1, 4)
+    a.mov64(2, src=6).add64(2, 32)
+    a.jmp(JGT, 2, "short", src=7)
+    a.ldx(8 if wide else 4, 8, 6, 0)
+    for reg, (off, size) in FIELDS.items():
+        a.ldx(size, reg, 6, off)
+    for k, (key, imms, verdict) in enumerate(rules):
+        nxt = f"r{k + 1}"
+        a.label(f"r{k}")
+        a.jmp(JNE, 8, nxt, imm=key, wide=wide)
+        for (reg, op, w), imm in zip(shape, imms):
+            a.jmp(op, reg, nxt, imm=imm, wide=w)
+        a.ja(f"v{verdict}")
+    a.label(f"r{len(rules)}").mov64(0, 7).exit()
+    for v in (1, 2, 3):
+        a.label(f"v{v}").mov64(0, v).exit()
+    a.label("short").mov64(0, 0).exit()
+    return a.assemble()
+
+
+def random_batch(seed, n):
+    from gobpfld_amd._native import np_dtypes
+    d_desc, _, _ = np_dtypes()
+    wide, shape, rules = random_rules(seed)
+    rng = np.random.default_rng(2000 + seed)
+    umem = rng.integers(0, 256, size=(n, 40), dtype=np.uint8)
+    for i in range(n):
+        if rng.random() < 0.8:
+            key, imms, _ = rules[int(rng.integers(0, len(rules)))]
+            umem[i, 0:8] = np.frombuffer(int(key & (2**64 - 1)).to_bytes(8, "little"), np.uint8)
+            for (reg, op, w), imm in zip(shape, imms):
+                if rng.random() < 0.5:  # the field near the rule's immediate
+                    off, size = FIELDS[reg]
+                    v = (imm + int(rng.integers(-2, 3))) & ((1 << (8 * size)) - 1)
+                    umem[i, off:off + size] = np.frombuffer(v.to_bytes(size, "little"), np.uint8)
+    descs = np.zeros(n, dtype=d_desc)
+    descs["addr"] = np.arange(n) * 40
+    descs["len"] = 40
+    return umem.reshape(-1).copy(), descs
+
+
+RANDOM_SEEDS = range(16)
+
+
+def test_random_chains_compile_as_dispatch():
+    from gobpfld_amd import aot
+    srcs = aot.sources([(prog_random(s), [], None, Settings(engine=ENGINE_JIT)) for s in RANDOM_SEEDS], variants=(0,))
+    assert sum("rule chain:" in x for x in srcs) == len(RANDOM_SEEDS), [("rule chain:" in x) for x in srcs]
+
+
+def test_random_chains_hostsim_equal_oracle(hostsim_lib, oracle_lib):
+    for seed in RANDOM_SEEDS:
+        umem, descs = random_batch(seed, 512)
+        assert_same(run_one(hostsim_lib, prog_random(seed), [], umem, descs),
+                    run_one(oracle_lib, prog_random(seed), [], umem, descs), f"seed {seed}")
+
+
+@pytest.mark.gpu
+def test_random_chains_device_equal_oracle(gpu_lib, oracle_lib):
+    """16 random chains (8-40 rules, 32- or 64-bit keys with repeats, 0-3 further tests of any jump op and
+    width) on the per-program kernels: results, registers and per-packet steps equal the oracle's walk."""
+    for seed in RANDOM_SEEDS:
+        umem, descs = random_batch(seed, 8192)
+        got = run_one(gpu_lib, prog_random(seed), [], umem, descs, settings=Settings(engine=ENGINE_JIT))
+        assert_same(got, run_one(oracle_lib, prog_random(seed), [], umem, descs), f"seed {seed}")
+        assert got[0].stats["engine_used"] == ENGINE_JIT

@@ -108,3 +108,29 @@ def test_segments_device_equal_oracle(gpu_lib, oracle_lib, name):
     for b, ((ga, gm), (wa, _)) in enumerate(zip(got, want)):
         assert_same(ga, wa, f"{name} batch {b}")
     assert got[0][1] in ((MODE_SEGMENTS, MODE_SEQUENTIAL) if name == "queue_drain_fast" else (MODE_SEGMENTS,)), got[0][1]
+
+
+def test_segments_async_stream_hostsim(hostsim_lib, oracle_lib):
+    """Pipelined batches (xe_run_batch_device_async): a batch that must be cut is completed through the
+    synchronous path, as segments, in submission order with the batches queued behind it."""
+    from parity import _dump, setup_one
+    prog, maps, entries = _case("queue_lru")
+    bs = [packets(2048, 64, seed=51 + b) for b in range(4)]
+    want = run_stream(oracle_lib, prog, maps, entries, Settings(), bs)
+    vm, idx = setup_one(hostsim_lib, prog, maps, Settings(), entries)
+    keep, handles = [], []
+    for u, d in bs:
+        u = u.copy()
+        v = np.zeros(len(d), dtype=np.uint32)
+        keep.append((u, v))
+        handles.append(vm.run_batch_device_async(u.ctypes.data, u.nbytes, d.ctypes.data, len(d), d_verdicts=v.ctypes.data))
+    sts = [h.stats() for h in handles]
+    dumps = [_dump(vm, m) for m in idx]
+    vm.close()
+    for b, ((r, _, _), _) in enumerate(want):
+        assert (keep[b][1] == r.verdicts).all(), f"batch {b}"
+    wd = want[-1][0][1]
+    assert dumps[1] == wd[1], "queue contents"
+    assert all(np.array_equal(dumps[0][k], wd[0][k]) if isinstance(dumps[0][k], np.ndarray) else dumps[0][k] == wd[0][k]
+               for k in dumps[0]), "LRU map"
+    assert sts[0]["mode_used"] == MODE_SEGMENTS

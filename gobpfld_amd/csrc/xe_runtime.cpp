@@ -2614,8 +2614,8 @@ void note_run(xe_vm* vm, const std::vector<unsigned long long>& red, uint32_t mo
 
 }  // namespace
 
-// Packet-order segments (XE_MODE_SEGMENTS): the batch's packets [0, cut) and [cut, n) as two batches, one
-// after the other (the second may be cut again), each through the whole path; their statistics summed.
+// Packet-order segments (XE_MODE_SEGMENTS): the batch's packets [0, cut), then windows of the rest, as
+// batches one after the other (any of them cut again), each through the whole path; statistics summed.
 // The failed pass is rolled back first exactly as for the in-order fallback (map values, packets, the
 // ordered maps' headers, LRU stamps and values from their snapshots), and each segment takes a new LRU
 // epoch, so its stamps order after the segment before it as packet order does. Not with a packet trace
@@ -2624,29 +2624,39 @@ constexpr uint32_t kSegMin = 64, kSegDepth = 64;
 static bool segments_ok(const xe_vm* vm, const XeParams& P) { return !P.trace && vm->seg_depth < kSegDepth; }
 static int run_segments(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* d_desc, uint32_t n, uint32_t cut,
                         void* d_results, void* d_verdicts, void* d_regs, void* stream, xe_batch_stats* stats) {
-  xe_batch_stats a{}, b{};
+  // [0, cut) ran exactly in the failed pass; after it, windows that double ([cut, 3 cut), ...), each a
+  // batch of its own (cut again inside when it must): the failed pass of a window covers that window,
+  // not all that follows, so a batch cut many times costs about one pass over it, not one per cut
   auto at = [](void* p, size_t k) -> void* { return p ? (void*)((uint8_t*)p + k) : nullptr; };
+  auto rank = [](uint32_t m) { return m == XE_MODE_SEQUENTIAL ? 3 : m == XE_MODE_KEYED ? 2 : 1; };
+  xe_batch_stats acc{};
+  acc.mode_used = XE_MODE_PARALLEL;
   vm->seg_depth++;
-  int rc = xe_run_batch_device(vm, d_umem, umem_len, d_desc, cut, d_results, d_verdicts, d_regs, stream, &a);
-  if (rc == XE_OK)
-    rc = xe_run_batch_device(vm, d_umem, umem_len, (const uint8_t*)d_desc + size_t(cut) * sizeof(xe_desc), n - cut,
-                             at(d_results, size_t(cut) * sizeof(xe_result)), at(d_verdicts, size_t(cut) * 4),
-                             at(d_regs, size_t(cut) * sizeof(xe_regs)), stream, &b);
+  int rc = XE_OK;
+  uint64_t pos = 0, len = cut;
+  while (rc == XE_OK && pos < n) {
+    xe_batch_stats b{};
+    rc = xe_run_batch_device(vm, d_umem, umem_len, (const uint8_t*)d_desc + size_t(pos) * sizeof(xe_desc), uint32_t(len),
+                             at(d_results, size_t(pos) * sizeof(xe_result)), at(d_verdicts, size_t(pos) * 4),
+                             at(d_regs, size_t(pos) * sizeof(xe_regs)), stream, &b);
+    acc.steps += b.steps;
+    for (int k = 0; k < 8; k++) acc.status_count[k] += b.status_count[k];
+    if (rank(b.mode_used) > rank(acc.mode_used)) acc.mode_used = b.mode_used;
+    acc.kernel_ms += b.kernel_ms;
+    acc.total_ms += b.total_ms;
+    acc.engine_used = b.engine_used;
+    acc.grid_blocks = std::max(acc.grid_blocks, b.grid_blocks);
+    pos += len;
+    len = std::min<uint64_t>(n - pos, 2 * len);
+  }
   vm->seg_depth--;
   if (rc != XE_OK) return rc;
   if (stats) {
+    *stats = acc;
     stats->packets = n;
-    stats->steps = a.steps + b.steps;
-    for (int k = 0; k < 8; k++) stats->status_count[k] = a.status_count[k] + b.status_count[k];
     // the slowest path any segment took; segments that all ran in parallel report XE_MODE_SEGMENTS
-    auto rank = [](uint32_t m) { return m == XE_MODE_SEQUENTIAL ? 3 : m == XE_MODE_KEYED ? 2 : 1; };
-    stats->mode_used = rank(a.mode_used) >= rank(b.mode_used) ? a.mode_used : b.mode_used;
     if (stats->mode_used == XE_MODE_PARALLEL) stats->mode_used = XE_MODE_SEGMENTS;
     stats->conflict = 1;
-    stats->kernel_ms = a.kernel_ms + b.kernel_ms;
-    stats->total_ms = a.total_ms + b.total_ms;
-    stats->engine_used = a.engine_used;
-    stats->grid_blocks = std::max(a.grid_blocks, b.grid_blocks);
   }
   return XE_OK;
 }
@@ -3197,12 +3207,14 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
     for (int attempt = 0;; attempt++) {
       if (ordmaps && ordered_hdr_read(vm, ord_h0, s)) return fail(vm, XE_ERR_DEVICE, "ordered map header");
       if (lists && list_init()) return fail(vm, XE_ERR_DEVICE, "list run");
+      tmark("ordered hdr");
       if (pops) {
         P.pop_mode = 1;
         P.popflag = vm->d_popflag;
         P.popbase = nullptr;
         if (dmemset(vm->d_popflag, 0, size_t(n) * 4, s)) return fail(vm, XE_ERR_DEVICE, "pop flags");
         if (int rc = pass()) return rc;
+        tmark("count pass");
         if (!conflict) {
           if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
           // Ranked passes: each popped list gets a slot; a packet's pops of it are counted in 8 bits of its
@@ -3237,9 +3249,11 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
                 return fail(vm, XE_ERR_DEVICE, "pop ranks");
             }
             if (rollback(false) || ordered_hdr_restore(vm, ord_h0, s) || list_init()) return fail(vm, XE_ERR_DEVICE, "pop ranks");
+            tmark("ranks");
             P.pop_mode = 2;
             P.popbase = vm->d_popbase;
             if (int rc = pass()) return rc;
+            tmark("ranked pass");
             if (conflict) break;
             if (list_read()) return fail(vm, XE_ERR_DEVICE, "list run");
             if (lr.newlist) {  // a pop of a list with no slot: rank it too
@@ -3302,6 +3316,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       break;
     }
     // (a segment costs a pass over what follows it: at least kSegMin packets, else the usual fallback)
+    tmark("passes done");
     if (conflict && mode == XE_MODE_AUTO && seg_cut >= kSegMin && seg_cut < n && segments_ok(vm, P)) {
       if (rollback(false) || (ordmaps && ordered_hdr_restore(vm, ord_h0, s))) return fail(vm, XE_ERR_DEVICE, "rollback");
       return run_segments(vm, d_umem, umem_len, d_desc, n, seg_cut, d_results, d_verdicts, d_regs, stream, stats);
@@ -3366,7 +3381,9 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
             j++;
           }
         }
+        tmark("before finalize");
         if (ordered_finalize(vm, h0, n, s)) return fail(vm, XE_ERR_DEVICE, "ordered map appends");
+        tmark("finalize");
         for (const auto& t : took) {
           HostMap& m = vm->maps[t.first];
           const uint64_t k = t.second;
@@ -3392,6 +3409,7 @@ int xe_run_batch_device(xe_vm* vm, void* d_umem, uint64_t umem_len, const void* 
       if (vm->maps[i].dkind == XE_DM_HASH) vm->maps[i].live = counts[i];
   }
   note_run(vm, red, used);
+  tmark("done");
   if (n > 0)  // an empty batch (a map upload) changes no map: the host mirrors stay current
     for (size_t i = 1; i < vm->maps.size(); i++) vm->maps[i].dev_dirty = true;
   if (stats) {

@@ -12,7 +12,8 @@ from gobpfld_amd.emulator import MODE_SEQUENTIAL, Settings
 from parity import assert_same, config_case, run_one
 
 N = 20000  # > 16,384: the scalar variant's threshold (xe_runtime.cpp kSeqScalarMin)
-CASES = {"c2": None, "c2rmw": None, "c3": 8192, "c3learn": 8192, "c3lru": 8192, "c5": 8192, "bpf2bpf": None}
+# (c4: the rule-chain dispatch, xe_jit.cpp rule_chain_at, in the scalar form: its table reads are uniform)
+CASES = {"c2": None, "c2rmw": None, "c3": 8192, "c3learn": 8192, "c3lru": 8192, "c4": None, "c5": 8192, "bpf2bpf": None}
 
 
 def cases():
